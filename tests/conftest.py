@@ -1,0 +1,26 @@
+"""Shared pytest configuration: the `gpu` marker and repo paths."""
+import os
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(REPO, "lzma-java_amd")
+for p in (REPO, PKG, os.path.join(REPO, "tests")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device)")
+
+
+def pytest_collection_modifyitems(config, items):
+    # gpu tests are selected explicitly with -m gpu; when a run selects them
+    # without a device present they must fail loudly, not skip silently.
+    pass
+
+
+@pytest.fixture(scope="session")
+def golden_dir():
+    return os.path.join(REPO, "tests", "golden")

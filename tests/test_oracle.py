@@ -1,0 +1,162 @@
+"""Pins the CPU restatement (oracle/) to the reference's own golden vectors.
+
+The reference is Java and no JDK exists here, so the oracle is pinned by:
+  * the 12 md5/length .lzma goldens of LzmaAloneTest.java:25-39 (firefox.exe),
+  * the range-coder known answers of RangeCoder/EncoderLearningTest.java:29-73,
+  * the bit-tree prices of BitTreeEncoderLearningTest.java:15-32.
+It also checks properties the GPU design relies on (two-phase match finding,
+SURVEY.md section 7.3) and decodability by an independent decoder (liblzma).
+"""
+import hashlib
+import json
+import lzma
+import os
+
+import numpy as np
+import pytest
+
+import oracle_ffi as orc
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _switch_params(switches):
+    p = dict(dict_size=1 << 23, fb=128, mf=1, lc=3, lp=0, pb=2, eos=0)   # LzmaAlone.java:24-37
+    for s in switches:
+        s = s[1:]
+        if s.startswith("fb"):
+            p["fb"] = int(s[2:])
+        elif s.startswith("lc"):
+            p["lc"] = int(s[2:])
+        elif s.startswith("lp"):
+            p["lp"] = int(s[2:])
+        elif s.startswith("pb"):
+            p["pb"] = int(s[2:])
+        elif s == "eos":
+            p["eos"] = 1
+        elif s == "mfbt2":
+            p["mf"] = 0
+        elif s.startswith("d"):
+            p["dict_size"] = 1 << int(s[1:])
+    return orc.params(**p)
+
+
+@pytest.fixture(scope="module")
+def firefox():
+    with open(os.path.join(GOLD, "firefox.exe"), "rb") as f:
+        data = f.read()
+    assert hashlib.md5(data).hexdigest() == "5744fff8e72d105c138dae9e17bb29fe"
+    return data
+
+
+with open(os.path.join(GOLD, "lzma_alone_goldens.json")) as f:
+    _GOLDENS = json.load(f)["cases"]
+
+
+@pytest.mark.parametrize("case", _GOLDENS, ids=[" ".join(c["switches"]) or "default" for c in _GOLDENS])
+def test_lzma_alone_golden(firefox, case):
+    p = _switch_params(case["switches"])
+    out = orc.lzma_file(firefox, p)
+    assert len(out) == case["len"]
+    assert hashlib.md5(out).hexdigest() == case["md5"]
+    # round trip through the Decoder restatement (LzmaAloneTest.java:54-55)
+    size = int.from_bytes(out[5:13], "little", signed=True)
+    rc, dec = orc.decode(out[13:], out[:5], size)
+    assert rc == 1 and dec == firefox
+
+
+with open(os.path.join(GOLD, "range_coder_known_answers.json")) as f:
+    _KAT = json.load(f)
+
+
+def _hex(b):
+    return " ".join("%02x" % x for x in b)
+
+
+@pytest.mark.parametrize("case", _KAT["encode_bits_prob_slot4"])
+def test_range_encoder_known_answers(case):
+    bits = np.array(case["bits"] or [0], dtype=np.int32)
+    out = np.zeros(64, dtype=np.uint8)
+    n = orc.lib().oracle_rc_encode_bits(bits.ctypes.data, len(case["bits"]), out.ctypes.data, 64)
+    assert _hex(out[:n]) == case["hex"]
+
+
+@pytest.mark.parametrize("case", _KAT["direct_bits"])
+def test_range_encoder_direct_bits(case):
+    vals = np.array([c[0] for c in case["calls"]], dtype=np.uint32)
+    nb = np.array([c[1] for c in case["calls"]], dtype=np.int32)
+    out = np.zeros(64, dtype=np.uint8)
+    n = orc.lib().oracle_rc_direct_bits(vals.ctypes.data, nb.ctypes.data, len(vals), out.ctypes.data, 64)
+    assert _hex(out[:n]) == case["hex"]
+
+
+def test_bittree_prices():
+    k = _KAT["bittree_prices_after_encode"]
+    prices = np.zeros(1 << k["num_bit_levels"], dtype=np.uint32)
+    orc.lib().oracle_bittree_prices_after(k["num_bit_levels"], k["encoded"], prices.ctypes.data)
+    assert prices.tolist() == k["prices"]
+
+
+def test_prob_prices_table_shape():
+    # ProbPrices.java:8-18: 512 entries, price(prob=1024) = 64 (one bit), monotone decreasing
+    lib = orc.lib()
+    t = [lib.oracle_prob_price(i) for i in range(512)]
+    assert t[256] == 64
+    assert all(t[i] >= t[i + 1] for i in range(1, 511))
+
+
+def _inputs():
+    rng = np.random.default_rng(7)
+    yield "empty", b""
+    yield "one", b"A"
+    yield "two", b"AB"
+    yield "run", b"\x00" * 5000
+    yield "rand", rng.integers(0, 256, 3000, dtype=np.uint8).tobytes()
+    words = [b"alpha", b"beta", b"gamma", b"delta", b"the", b" ", b"\n"]
+    yield "text", b"".join(words[i] for i in rng.integers(0, len(words), 4000))
+    yield "period", (b"abcdefghij" * 700)[:6999]
+    yield "lowent", rng.integers(0, 4, 20000, dtype=np.uint8).tobytes()
+
+
+_PARAMS = [
+    dict(dict_size=1 << 16, fb=32, mf=1),
+    dict(dict_size=1 << 12, fb=5, mf=0),
+    dict(dict_size=1 << 20, fb=273, mf=1, lc=0, lp=2, pb=0),
+    dict(dict_size=100, fb=64, mf=2, eos=1),
+    dict(dict_size=1, fb=16, mf=1),
+]
+
+
+@pytest.mark.parametrize("pi", range(len(_PARAMS)))
+def test_two_phase_match_finding_equals_reference_order(pi):
+    """Precomputing fillMatches at every position (phase 1) and then parsing
+    (phase 2) gives the reference's bits: Skip and fillMatches make identical
+    tree updates (BinTree.java:249-256 vs 335-339), SURVEY.md section 7.3."""
+    p = orc.params(**_PARAMS[pi])
+    for name, data in _inputs():
+        a = orc.encode(data, p, mode=0)
+        b = orc.encode(data, p, mode=1)
+        assert a == b, name
+
+
+@pytest.mark.parametrize("pi", range(len(_PARAMS)))
+def test_roundtrip_and_liblzma_cross_check(pi):
+    p = orc.params(**_PARAMS[pi])
+    for name, data in _inputs():
+        f = orc.lzma_file(data, p)
+        size = -1 if p.eos else len(data)
+        rc, dec = orc.decode(f[13:], f[:5], size)
+        assert rc == 1 and dec == data, name
+        if p.lc + p.lp <= 4:   # liblzma rejects lc+lp > 4 in FORMAT_ALONE
+            assert lzma.decompress(f, format=lzma.FORMAT_ALONE) == data, name
+
+
+def test_decoder_rejects_corrupt_distance():
+    # first symbol a match => rep0 >= nowPos => Decoder.Code returns false (Decoder.java:288-291)
+    rng = np.random.default_rng(3)
+    bad = 0
+    for _ in range(50):
+        junk = bytes([0]) + rng.integers(0, 256, 64, dtype=np.uint8).tobytes()
+        rc, _ = orc.decode(junk, bytes([0x5D, 0, 0, 0, 1]), 1000)
+        bad += rc == 0
+    assert bad > 0
