@@ -1,0 +1,115 @@
+/*
+ * lzma_mi355x.h -- C ABI of the MI355X-native LZMA encode/decode path.
+ *
+ * This is the drop-in boundary for the hot path of rfalke/lzma-java
+ * (src/main/java/SevenZip/Compression/LZMA/Encoder.java and Decoder.java).
+ * Plain C types only: no torch, no HIP types in the signatures (streams are
+ * passed as void*). A JNI shim binds these entry points
+ * for the Java drop-in classes SevenZip.Compression.LZMA.Encoder/Decoder.
+ *
+ * Reference interface each entry point replaces:
+ *   lzma_params_default   Encoder() field defaults          Encoder.java:135-160
+ *   lzma_params_check     Encoder setters' range checks      Encoder.java:1135-1180
+ *   lzma_write_props      Encoder.WriteCoderProperties       Encoder.java:1079-1085
+ *   lzma_read_props       Decoder.SetDecoderProperties       Decoder.java:303-318
+ *   lzma_encode           Encoder.Code (one stream)          Encoder.java:1064-1077
+ *   lzma_enc_batch[_dev]  Encoder.Code on N independent streams
+ *   lzma_decode           Decoder.Code (one stream)          Decoder.java:205-301
+ *   lzma_dec_batch[_dev]  Decoder.Code on N independent streams
+ *   lzma_bench_generate   LzmaBench.CBenchRandomGenerator    LzmaBench.java:15-127
+ *
+ * Every encoded stream is byte-identical to Encoder.Code on the same bytes
+ * with the same parameters: raw range-coder bytes, no 13-byte .lzma header
+ * (the header is written by the caller, LzmaAlone.java:208-217).
+ * Errors are returned as status codes; nothing throws across the ABI.
+ */
+#ifndef LZMA_MI355X_H
+#define LZMA_MI355X_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LZMA_OK 0
+#define LZMA_E_PARAM (-1)     /* a setter would have returned false */
+#define LZMA_E_NOMEM (-2)     /* host or device allocation failed */
+#define LZMA_E_DEVICE (-3)    /* HIP runtime error */
+#define LZMA_E_OVERFLOW (-4)  /* output capacity too small */
+#define LZMA_E_DATA (-5)      /* corrupt stream: Decoder.Code returned false */
+#define LZMA_E_NODEVICE (-6)  /* no HIP device: the product path has no CPU fallback */
+#define LZMA_E_INTERNAL (-7)
+
+typedef struct lzma_params {
+    int32_t dict_size; /* 1 .. 2^29            (Encoder.SetDictionarySize) */
+    int32_t fb;        /* 5 .. 273             (Encoder.SetNumFastBytes) */
+    int32_t mf;        /* 0=bt2 1=bt4 2=bt4b   (Encoder.SetMatchFinder) */
+    int32_t lc;        /* 0 .. 8               (Encoder.SetLcLpPb) */
+    int32_t lp;        /* 0 .. 4 */
+    int32_t pb;        /* 0 .. 4 */
+    int32_t eos;       /* end marker           (Encoder.SetEndMarkerMode) */
+} lzma_params;
+
+typedef struct lzma_ctx lzma_ctx;
+
+const char *lzma_version(void);
+int lzma_params_default(lzma_params *p);
+int lzma_params_check(const lzma_params *p);
+int lzma_write_props(const lzma_params *p, uint8_t out[5]);
+int lzma_read_props(const uint8_t in[5], lzma_params *p);
+/* Output capacity that always suffices for one encoded stream of n bytes. */
+uint64_t lzma_enc_bound(uint64_t n);
+
+int lzma_ctx_create(int device, lzma_ctx **out);
+void lzma_ctx_destroy(lzma_ctx *ctx);
+const char *lzma_last_error(const lzma_ctx *ctx);
+/* Upper bound on input bytes processed per device pass (workspace sizing). */
+int lzma_ctx_set_batch_bytes(lzma_ctx *ctx, uint64_t bytes);
+/* Per-kernel timing with HIP events on the launch stream (0 = off). */
+int lzma_ctx_set_timing(lzma_ctx *ctx, int on);
+/* names[i] / ms[i] / launches[i] for up to cap kernels; returns count. */
+int lzma_ctx_timings(lzma_ctx *ctx, const char **names, double *ms, int64_t *launches, int cap);
+void lzma_ctx_reset_timings(lzma_ctx *ctx);
+
+/* ---- encode -------------------------------------------------------------
+ * Device-resident batch: stream i is d_in[h_offs[i] .. h_offs[i+1]).
+ * Output region i is d_out[h_out_offs[i] .. h_out_offs[i+1]) (capacity,
+ * use lzma_enc_bound); h_out_lens[i] receives the encoded length.
+ * hip_stream: a hipStream_t or NULL. Returns LZMA_OK or an error code. */
+int lzma_enc_batch_dev(lzma_ctx *ctx, const lzma_params *p,
+                       const uint8_t *d_in, const uint64_t *h_offs, int nstreams,
+                       uint8_t *d_out, const uint64_t *h_out_offs, uint64_t *h_out_lens,
+                       void *hip_stream);
+/* Host buffers: out is packed, out_offs[nstreams+1] receives the layout. */
+int lzma_enc_batch(lzma_ctx *ctx, const lzma_params *p,
+                   const uint8_t *in, const uint64_t *offs, int nstreams,
+                   uint8_t *out, uint64_t out_cap, uint64_t *out_offs);
+/* One stream: Encoder.Code(in, out, -1, -1, null). */
+int lzma_encode(lzma_ctx *ctx, const lzma_params *p, const uint8_t *in, uint64_t n,
+                uint8_t *out, uint64_t out_cap, uint64_t *out_len);
+
+/* ---- decode -------------------------------------------------------------
+ * props: the 5 property bytes (Decoder.SetDecoderProperties).
+ * h_out_sizes[i] = outSize of Decoder.Code (-1 => until end marker).
+ * h_status[i] = LZMA_OK, LZMA_E_DATA (Decoder.Code false) or LZMA_E_OVERFLOW. */
+int lzma_dec_batch_dev(lzma_ctx *ctx, const uint8_t props[5],
+                       const uint8_t *d_in, const uint64_t *h_in_offs, int nstreams,
+                       const int64_t *h_out_sizes,
+                       uint8_t *d_out, const uint64_t *h_out_offs, uint64_t *h_out_lens,
+                       int32_t *h_status, void *hip_stream);
+int lzma_dec_batch(lzma_ctx *ctx, const uint8_t props[5],
+                   const uint8_t *in, const uint64_t *in_offs, int nstreams,
+                   const int64_t *out_sizes, uint8_t *out, const uint64_t *out_offs,
+                   uint64_t *out_lens, int32_t *status);
+int lzma_decode(lzma_ctx *ctx, const uint8_t props[5], const uint8_t *in, uint64_t n,
+                int64_t out_size, uint8_t *out, uint64_t out_cap, uint64_t *out_len);
+
+/* ---- synthetic inputs (bench / tests) ----------------------------------- */
+/* LzmaBench.CBenchRandomGenerator.Generate (LzmaBench.java:104-127). */
+void lzma_bench_generate(uint8_t *buf, uint64_t size);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LZMA_MI355X_H */

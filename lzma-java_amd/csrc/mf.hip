@@ -1,0 +1,338 @@
+// mf.hip -- phase 1 of the encoder: the BT2/BT4 binary-tree match finder of
+// src/main/java/SevenZip/Compression/LZ/BinTree.java, computed for every
+// position of a batch of independent streams at once.
+//
+// Why this is legal: the match list of position P depends
+// only on (input, dict, fb, mf), never on parser decisions, because Skip and
+// fillMatches make identical tree updates (BinTree.java:249-256 vs 335-339).
+// A position's tree only ever links positions of the same hash4 bucket, so
+// every bucket is an independent sequential simulation:
+//   K1 mf_keys     hash every position (BinTree.java:170-178), key = (stream, hv)
+//   K2 radix sort  (stream, hv) stable => each bucket a contiguous, position-
+//                  ordered segment; hash2/hash3 "last occurrence" likewise
+//   K3 mf_links    prev-in-bucket for hash2/hash3; bucket (chain) heads
+//   K4 mf_walk     one lane per bucket: replays BinTree.fillMatches0
+//                  (:152-273) for the bucket's positions in order, with the
+//                  son[] links indexed by absolute position (window expiry
+//                  via matchMinPos makes cyclic reuse unobservable).
+// Output per position: minfo = count | main_len << 16 (main_len = longest
+// pair extended past fb as Encoder.ReadMatchDistances does, Encoder.java:
+// 275-287), kInlinePairs packed pairs inline, the rest in an overflow pool.
+#include <hipcub/hipcub.hpp>
+
+#include "lzma_common.h"
+#include "runtime.h"
+
+namespace lzg {
+
+static __constant__ Tables c_tab = make_tables();
+
+constexpr uint64_t kSentinel = ~0ull;
+
+__device__ inline int find_stream(const uint64_t* offs, int nstreams, uint64_t g) {
+    // largest s with offs[s] <= g (offs has nstreams+1 entries, offs[nstreams] = total)
+    int lo = 0, hi = nstreams;  // answer in [lo, hi)
+    while (hi - lo > 1) {
+        int mid = (lo + hi) >> 1;
+        if (offs[mid] <= g) lo = mid; else hi = mid;
+    }
+    return lo;
+}
+
+template <bool BT4>
+__global__ void __launch_bounds__(256) mf_keys_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ offs,
+                                                      int nstreams, uint64_t total, MfArgs a) {
+    for (uint64_t g = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; g < total; g += (uint64_t)gridDim.x * blockDim.x) {
+        int s = find_stream(offs, nstreams, g);
+        uint64_t base = offs[s], n = offs[s + 1] - base, p = g - base;
+        a.minfo[g] = 0;
+        a.vals[g] = (uint32_t)g;
+        uint64_t rem = n - p;
+        uint32_t len_limit = rem < a.fb ? (uint32_t)rem : a.fb;
+        if (len_limit < a.min_match_check) {   // BinTree.java:153-162: no insertion
+            a.k4[g] = kSentinel;
+            if (BT4) { a.k3[g] = kSentinel; a.k2[g] = kSentinel; }
+            continue;
+        }
+        uint32_t b0 = in[g], b1 = in[g + 1];
+        if (BT4) {
+            uint32_t b2 = in[g + 2], b3 = in[g + 3];
+            uint32_t temp = c_tab.crc[b0] ^ b1;
+            uint32_t h2 = temp & 1023u;
+            temp ^= b2 << 8;
+            uint32_t h3 = temp & 0xFFFFu;
+            uint32_t hv = (temp ^ (c_tab.crc[b3] << 5)) & a.hash_mask;
+            a.k4[g] = ((uint64_t)s << a.hash_bits) | hv;
+            a.k3[g] = ((uint64_t)s << 16) | h3;
+            a.k2[g] = ((uint64_t)s << 10) | h2;
+        } else {
+            a.k4[g] = ((uint64_t)s << 16) | (b0 ^ (b1 << 8));
+        }
+    }
+}
+
+// prev-in-bucket for a position-ordered sorted key array (hash2 / hash3 heads)
+__global__ void __launch_bounds__(256) mf_prev_kernel(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ vals,
+                                                      uint64_t total, uint32_t* __restrict__ prev) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < total; i += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t k = keys[i];
+        if (k == kSentinel) continue;
+        prev[vals[i]] = (i > 0 && keys[i - 1] == k) ? vals[i - 1] : kNoPos;
+    }
+}
+
+// chain heads of the hash4 sort + number of valid (non-sentinel) entries
+__global__ void __launch_bounds__(256) mf_heads_kernel(const uint64_t* __restrict__ keys, uint64_t total,
+                                                       uint8_t* __restrict__ flag, uint64_t* __restrict__ nvalid) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < total; i += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t k = keys[i];
+        bool valid = k != kSentinel;
+        flag[i] = valid && (i == 0 || keys[i - 1] != k);
+        if (valid && (i + 1 == total || keys[i + 1] == kSentinel)) *nvalid = i + 1;
+    }
+}
+
+__global__ void __launch_bounds__(256) mf_chain_len_kernel(const uint32_t* __restrict__ starts, const uint64_t* __restrict__ nchains_p,
+                                                           const uint64_t* __restrict__ nvalid_p, uint32_t* __restrict__ lens) {
+    uint64_t nchains = *nchains_p, nvalid = *nvalid_p;
+    for (uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; c < nchains; c += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t e = (c + 1 < nchains) ? starts[c + 1] : nvalid;
+        lens[c] = (uint32_t)(e - starts[c]);
+    }
+}
+
+// Unaligned 8-byte little-endian load from a buffer padded by >= 16 bytes.
+__device__ inline uint64_t load8(const uint8_t* p) {
+    uintptr_t a = (uintptr_t)p;
+    const uint64_t* q = (const uint64_t*)(a & ~(uintptr_t)7);
+    uint32_t sh = (uint32_t)(a & 7) * 8;
+    uint64_t lo = q[0], hi = q[1];
+    return sh ? (lo >> sh) | (hi << (64 - sh)) : lo;
+}
+
+// Common-prefix length of a[0..limit) and b[0..limit), starting at `from`.
+__device__ inline uint32_t common_len(const uint8_t* a, const uint8_t* b, uint32_t from, uint32_t limit) {
+    uint32_t len = from;
+    while (len < limit) {
+        uint64_t x = load8(a + len) ^ load8(b + len);
+        if (x) {
+            uint32_t r = len + (uint32_t)(__builtin_ctzll(x) >> 3);
+            return r < limit ? r : limit;
+        }
+        len += 8;
+    }
+    return limit;
+}
+
+template <typename PairT, bool BT4>
+__global__ void __launch_bounds__(64) mf_walk_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ offs,
+                                                     const uint64_t* __restrict__ keys4, const uint32_t* __restrict__ vals4,
+                                                     const uint32_t* __restrict__ chain_order,
+                                                     const uint32_t* __restrict__ chain_start,
+                                                     const uint32_t* __restrict__ chain_len,
+                                                     const uint64_t* __restrict__ nchains_p,
+                                                     MfArgs a, uint32_t* __restrict__ son, PairT* __restrict__ pairs,
+                                                     uint32_t* __restrict__ ovf_off, PairT* __restrict__ ovf,
+                                                     unsigned long long* __restrict__ ovf_used, uint64_t ovf_cap,
+                                                     int* __restrict__ err) {
+    using PP = PairPack<PairT>;
+    uint64_t nchains = *nchains_p;
+    uint64_t ci = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (ci >= nchains) return;
+    uint32_t c = chain_order[ci];
+    uint64_t start = chain_start[c], end = start + chain_len[c];
+    uint64_t key = keys4[start];
+    int s = (int)(key >> (BT4 ? a.hash_bits : 16));
+    uint64_t base = offs[s], n = offs[s + 1] - base;
+    const uint8_t* sb = in + base;          // stream bytes, 0-based
+    const uint32_t fb = a.fb, cut = a.cut_value;
+    const uint64_t cyc = a.cyc_size;
+    uint32_t prev_local = 0;                // 1-based local position of previous bucket member, 0 = none
+    for (uint64_t i = start; i < end; i++) {
+        uint64_t g = vals4[i];
+        uint32_t p = (uint32_t)(g - base);
+        uint32_t pos = p + 1;               // BinTree 1-based position
+        uint64_t rem = n - p;
+        uint32_t len_limit = rem < fb ? (uint32_t)rem : fb;
+        uint32_t match_min = (uint64_t)pos > cyc ? (uint32_t)(pos - cyc) : 0;
+        const uint8_t* cur = sb + p;
+        uint32_t cur_match = prev_local;
+        uint32_t max_len = 1, cnt = 0;
+        PairT* inl = pairs + g * kInlinePairs;
+        PairT* ov = nullptr;
+        auto emit = [&](uint32_t l, uint32_t d) {
+            if (cnt < kInlinePairs) {
+                inl[cnt] = PP::pack(l, d);
+            } else {
+                if (ov == nullptr) {
+                    unsigned long long o = atomicAdd(ovf_used, (unsigned long long)(fb + 2));
+                    if (o + fb + 2 > ovf_cap) { *err = 1; o = 0; }
+                    ovf_off[g] = (uint32_t)o;
+                    ov = ovf + o;
+                }
+                if (!*err) ov[cnt - kInlinePairs] = PP::pack(l, d);
+            }
+            cnt++;
+        };
+        if (BT4) {   // hash2 / hash3 candidates, BinTree.java:183-207
+            uint32_t pv2 = a.prev2[g], pv3 = a.prev3[g];
+            uint32_t cm2 = pv2 == kNoPos ? 0 : (uint32_t)(pv2 - base) + 1;
+            uint32_t cm3 = pv3 == kNoPos ? 0 : (uint32_t)(pv3 - base) + 1;
+            if (cm2 > match_min && sb[cm2 - 1] == cur[0]) { max_len = 2; emit(2, pos - cm2 - 1); }
+            if (cm3 > match_min && sb[cm3 - 1] == cur[0]) {
+                if (cm3 == cm2) cnt--;
+                max_len = 3;
+                emit(3, pos - cm3 - 1);
+                cm2 = cm3;
+            }
+            if (cnt != 0 && cm2 == cur_match) { cnt--; max_len = 1; }
+        }
+        uint64_t ptr0 = 2 * g + 1, ptr1 = 2 * g;
+        uint32_t len0 = a.direct_bytes, len1 = a.direct_bytes;
+        if (!BT4 && cur_match > match_min) {   // BT2 direct byte check, BinTree.java:218-226
+            if (sb[cur_match - 1 + 2] != cur[2]) { max_len = 2; emit(2, pos - cur_match - 1); }
+        }
+        uint32_t count = cut;
+        for (;;) {   // BinTree.java:230-270
+            if (cur_match <= match_min || count-- == 0) { son[ptr0] = 0; son[ptr1] = 0; break; }
+            uint32_t delta = pos - cur_match;
+            uint64_t cp = 2 * (base + cur_match - 1);
+            const uint8_t* pby = sb + (cur_match - 1);
+            uint32_t len = len0 < len1 ? len0 : len1;
+            if (pby[len] == cur[len]) {
+                len = common_len(pby, cur, len + 1, len_limit);
+                if (max_len < len) {
+                    max_len = len;
+                    emit(len, delta - 1);
+                    if (len == len_limit) { son[ptr1] = son[cp]; son[ptr0] = son[cp + 1]; break; }
+                }
+            }
+            if (pby[len] < cur[len]) { son[ptr1] = cur_match; ptr1 = cp + 1; cur_match = son[ptr1]; len1 = len; }
+            else { son[ptr0] = cur_match; ptr0 = cp; cur_match = son[ptr0]; len0 = len; }
+        }
+        uint32_t ml = 0;
+        if (cnt > 0) {   // Encoder.ReadMatchDistances extension, Encoder.java:279-284
+            PairT last = cnt <= kInlinePairs ? inl[cnt - 1] : ov[cnt - 1 - kInlinePairs];
+            ml = PP::len(last);
+            if (ml == fb) {
+                uint32_t d1 = PP::dist(last) + 1;
+                uint64_t from = (uint64_t)p + ml;
+                uint64_t lim = kMatchMaxLen - ml;
+                if (from + lim > n) lim = n - from;
+                ml += common_len(sb + from - d1, sb + from, 0, (uint32_t)lim);
+            }
+        }
+        a.minfo[g] = cnt | (ml << 16);
+        prev_local = pos;
+    }
+}
+
+// ----------------------------------------------------------------- host side
+
+static inline uint32_t bits_for(uint64_t v) { uint32_t b = 0; while (b < 64 && (v >> b) != 0) b++; return b; }
+
+template <typename KeyT, typename ValT>
+static int radix_sort(Ctx* ctx, const KeyT* kin, KeyT* kout, const ValT* vin, ValT* vout, uint64_t n, int end_bit,
+                      hipStream_t st, bool descending = false) {
+    size_t tmp = 0;
+    hipError_t e;
+    if (descending)
+        e = hipcub::DeviceRadixSort::SortPairsDescending(nullptr, tmp, kin, kout, vin, vout, (int)n, 0, end_bit, st);
+    else
+        e = hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, kin, kout, vin, vout, (int)n, 0, end_bit, st);
+    if (e != hipSuccess) return ctx->fail(LZMA_E_DEVICE, "radix sort sizing: %s", hipGetErrorString(e));
+    void* t = ctx->scratch(tmp);
+    if (!t && tmp) return ctx->fail(LZMA_E_NOMEM, "radix sort temp %zu", tmp);
+    if (descending)
+        e = hipcub::DeviceRadixSort::SortPairsDescending(t, tmp, kin, kout, vin, vout, (int)n, 0, end_bit, st);
+    else
+        e = hipcub::DeviceRadixSort::SortPairs(t, tmp, kin, kout, vin, vout, (int)n, 0, end_bit, st);
+    if (e != hipSuccess) return ctx->fail(LZMA_E_DEVICE, "radix sort: %s", hipGetErrorString(e));
+    return LZMA_OK;
+}
+
+static inline unsigned grid_for(uint64_t n, unsigned block, unsigned cap = 65536) {
+    uint64_t g = (n + block - 1) / block;
+    if (g < 1) g = 1;
+    return (unsigned)(g < cap ? g : cap);
+}
+
+// Runs K1..K4 for one batch. in: padded device copy of the batch; offs: device
+// stream offsets (nstreams+1). Fills w.minfo / w.pairs / w.ovf_off / w.ovf.
+int run_match_finder(Ctx* ctx, const Derived& d, const uint8_t* in, const uint64_t* d_offs, int nstreams,
+                     uint64_t total, bool wide_pairs, MfBuffers& w, hipStream_t st) {
+    if (total == 0) return LZMA_OK;
+    if (total >= 0xFFFFFFFFull) return ctx->fail(LZMA_E_PARAM, "batch too large for 32-bit positions");
+    MfArgs a{};
+    a.fb = d.fb; a.min_match_check = d.min_match_check; a.hash_mask = d.hash_mask; a.hash_bits = d.hash_bits;
+    a.cut_value = d.cut_value; a.cyc_size = d.cyc_size; a.direct_bytes = d.direct_bytes;
+    a.k4 = w.k4; a.k3 = w.k3; a.k2 = w.k2; a.vals = w.vals; a.minfo = w.minfo; a.prev2 = w.prev2; a.prev3 = w.prev3;
+    const bool bt4 = d.hash_array != 0;
+    const unsigned B = 256;
+    const uint32_t sbits = bits_for((uint64_t)nstreams) + 1;
+    {
+        TimedLaunch tl(ctx, "mf_keys", st);
+        if (bt4) hipLaunchKernelGGL((mf_keys_kernel<true>), dim3(grid_for(total, B)), dim3(B), 0, st, in, d_offs, nstreams, total, a);
+        else hipLaunchKernelGGL((mf_keys_kernel<false>), dim3(grid_for(total, B)), dim3(B), 0, st, in, d_offs, nstreams, total, a);
+    }
+    int rc;
+    if (bt4) {
+        {
+            TimedLaunch tl(ctx, "mf_sort", st);
+            if ((rc = radix_sort(ctx, w.k2, w.ks, w.vals, w.vs, total, (int)(10 + sbits), st))) return rc;
+        }
+        hipLaunchKernelGGL(mf_prev_kernel, dim3(grid_for(total, B)), dim3(B), 0, st, w.ks, w.vs, total, w.prev2);
+        {
+            TimedLaunch tl(ctx, "mf_sort", st);
+            if ((rc = radix_sort(ctx, w.k3, w.ks, w.vals, w.vs, total, (int)(16 + sbits), st))) return rc;
+        }
+        hipLaunchKernelGGL(mf_prev_kernel, dim3(grid_for(total, B)), dim3(B), 0, st, w.ks, w.vs, total, w.prev3);
+    }
+    {
+        TimedLaunch tl(ctx, "mf_sort", st);
+        if ((rc = radix_sort(ctx, w.k4, w.ks, w.vals, w.vs, total, (int)((bt4 ? d.hash_bits : 16) + sbits), st))) return rc;
+    }
+    hipMemsetAsync(w.counts, 0, 2 * sizeof(uint64_t), st);   // [0]=nvalid [1]=nchains
+    hipLaunchKernelGGL(mf_heads_kernel, dim3(grid_for(total, B)), dim3(B), 0, st, w.ks, total, w.flag, w.counts);
+    {
+        size_t tmp = 0;
+        hipcub::CountingInputIterator<uint32_t> it(0);
+        hipcub::DeviceSelect::Flagged(nullptr, tmp, it, w.flag, w.chain_start, w.counts + 1, (int)total, st);
+        void* t = ctx->scratch(tmp);
+        if (!t && tmp) return ctx->fail(LZMA_E_NOMEM, "select temp");
+        hipcub::DeviceSelect::Flagged(t, tmp, it, w.flag, w.chain_start, w.counts + 1, (int)total, st);
+    }
+    uint64_t hc[2];
+    hipMemcpyAsync(hc, w.counts, sizeof(hc), hipMemcpyDeviceToHost, st);
+    if (hipStreamSynchronize(st) != hipSuccess) return ctx->fail(LZMA_E_DEVICE, "sync after chain select");
+    uint64_t nchains = hc[1];
+    if (nchains == 0) return LZMA_OK;
+    hipLaunchKernelGGL(mf_chain_len_kernel, dim3(grid_for(nchains, B)), dim3(B), 0, st, w.chain_start, w.counts + 1, w.counts, w.chain_len);
+    // longest chains first so lanes of one wave walk similar-length buckets
+    {
+        TimedLaunch tl(ctx, "mf_sort", st);
+        hipLaunchKernelGGL(iota_kernel, dim3(grid_for(nchains, B)), dim3(B), 0, st, w.chain_idx, nchains);
+        if ((rc = radix_sort(ctx, w.chain_len, w.chain_len_sorted, w.chain_idx, w.chain_order, nchains, 32, st, true))) return rc;
+    }
+    hipMemsetAsync(w.ovf_used, 0, sizeof(unsigned long long), st);
+    hipMemsetAsync(w.err, 0, sizeof(int), st);
+    {
+        TimedLaunch tl(ctx, "mf_walk", st);
+        const unsigned WB = 64;
+        unsigned grid = (unsigned)((nchains + WB - 1) / WB);
+        if (wide_pairs) {
+            if (bt4) hipLaunchKernelGGL((mf_walk_kernel<uint64_t, true>), dim3(grid), dim3(WB), 0, st, in, d_offs, w.ks, w.vs, w.chain_order, w.chain_start, w.chain_len, w.counts + 1, a, w.son, (uint64_t*)w.pairs, w.ovf_off, (uint64_t*)w.ovf, w.ovf_used, w.ovf_cap, w.err);
+            else hipLaunchKernelGGL((mf_walk_kernel<uint64_t, false>), dim3(grid), dim3(WB), 0, st, in, d_offs, w.ks, w.vs, w.chain_order, w.chain_start, w.chain_len, w.counts + 1, a, w.son, (uint64_t*)w.pairs, w.ovf_off, (uint64_t*)w.ovf, w.ovf_used, w.ovf_cap, w.err);
+        } else {
+            if (bt4) hipLaunchKernelGGL((mf_walk_kernel<uint32_t, true>), dim3(grid), dim3(WB), 0, st, in, d_offs, w.ks, w.vs, w.chain_order, w.chain_start, w.chain_len, w.counts + 1, a, w.son, (uint32_t*)w.pairs, w.ovf_off, (uint32_t*)w.ovf, w.ovf_used, w.ovf_cap, w.err);
+            else hipLaunchKernelGGL((mf_walk_kernel<uint32_t, false>), dim3(grid), dim3(WB), 0, st, in, d_offs, w.ks, w.vs, w.chain_order, w.chain_start, w.chain_len, w.counts + 1, a, w.son, (uint32_t*)w.pairs, w.ovf_off, (uint32_t*)w.ovf, w.ovf_used, w.ovf_cap, w.err);
+        }
+    }
+    int herr = 0;
+    hipMemcpyAsync(&herr, w.err, sizeof(int), hipMemcpyDeviceToHost, st);
+    if (hipStreamSynchronize(st) != hipSuccess) return ctx->fail(LZMA_E_DEVICE, "mf_walk: %s", hipGetErrorString(hipGetLastError()));
+    if (herr) return LZMA_E_OVERFLOW;   // caller grows the overflow pool and retries
+    return LZMA_OK;
+}
+
+}  // namespace lzg

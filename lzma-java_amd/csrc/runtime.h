@@ -1,0 +1,192 @@
+// runtime.h -- device context, workspace arena, per-kernel HIP-event timing and
+// the argument blocks shared by the kernels and the host orchestration.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdarg.h>
+#include <stdint.h>
+#include <stdio.h>
+
+#include <map>
+#include <string>
+#include <vector>
+
+#include "lzma_common.h"
+
+namespace lzg {
+
+struct MfArgs {
+    uint32_t fb, min_match_check, hash_mask, hash_bits, cut_value, direct_bytes;
+    uint64_t cyc_size;
+    uint64_t *k4, *k3, *k2;
+    uint32_t *vals, *minfo, *prev2, *prev3;
+};
+
+struct MfBuffers {
+    uint64_t *k4, *k3, *k2, *ks;
+    uint32_t *vals, *vs, *minfo, *prev2, *prev3;
+    uint8_t* flag;
+    uint32_t *chain_start, *chain_len, *chain_len_sorted, *chain_idx, *chain_order;
+    uint64_t* counts;
+    uint32_t* son;
+    void* pairs;
+    uint32_t* ovf_off;
+    void* ovf;
+    uint64_t ovf_cap;
+    unsigned long long* ovf_used;
+    int* err;
+};
+
+struct Ctx;
+
+struct TimedLaunch {
+    Ctx* ctx;
+    const char* name;
+    hipStream_t st;
+    hipEvent_t a = nullptr, b = nullptr;
+    TimedLaunch(Ctx* c, const char* n, hipStream_t s);
+    ~TimedLaunch();
+};
+
+struct Ctx {
+    int device = 0;
+    std::string err;
+    uint64_t batch_bytes = 512ull << 20;
+    // persistent workspace arena (grown, never shrunk)
+    uint8_t* arena = nullptr;
+    size_t arena_size = 0;
+    uint8_t* tmp = nullptr;     // cub temp storage
+    size_t tmp_size = 0;
+    uint64_t ovf_hint = 0;      // overflow pool slots per byte * 1024 (grows on retry)
+    // timing
+    bool timing = false;
+    struct Pending { std::string name; hipEvent_t a, b; };
+    std::vector<Pending> pending;
+    std::vector<hipEvent_t> free_events;
+    struct Acc { double ms = 0; int64_t n = 0; };
+    std::map<std::string, Acc> acc;
+
+    int fail(int code, const char* fmt, ...) {
+        char buf[512];
+        va_list ap;
+        va_start(ap, fmt);
+        vsnprintf(buf, sizeof buf, fmt, ap);
+        va_end(ap);
+        err = buf;
+        return code;
+    }
+    void* scratch(size_t n) {
+        if (n == 0) return tmp;
+        if (n > tmp_size) {
+            if (tmp) hipFree(tmp);
+            tmp = nullptr;
+            tmp_size = 0;
+            if (hipMalloc(&tmp, n) != hipSuccess) return nullptr;
+            tmp_size = n;
+        }
+        return tmp;
+    }
+    bool ensure_arena(size_t n) {
+        if (n <= arena_size) return true;
+        if (arena) hipFree(arena);
+        arena = nullptr;
+        arena_size = 0;
+        if (hipMalloc(&arena, n) != hipSuccess) return false;
+        arena_size = n;
+        return true;
+    }
+    hipEvent_t get_event() {
+        if (!free_events.empty()) { hipEvent_t e = free_events.back(); free_events.pop_back(); return e; }
+        hipEvent_t e;
+        hipEventCreate(&e);
+        return e;
+    }
+    void resolve_timings() {
+        for (auto& p : pending) {
+            hipEventSynchronize(p.b);
+            float ms = 0;
+            hipEventElapsedTime(&ms, p.a, p.b);
+            Acc& a = acc[p.name];
+            a.ms += ms;
+            a.n += 1;
+            free_events.push_back(p.a);
+            free_events.push_back(p.b);
+        }
+        pending.clear();
+    }
+};
+
+inline TimedLaunch::TimedLaunch(Ctx* c, const char* n, hipStream_t s) : ctx(c), name(n), st(s) {
+    if (ctx->timing) { a = ctx->get_event(); b = ctx->get_event(); hipEventRecord(a, st); }
+}
+inline TimedLaunch::~TimedLaunch() {
+    if (ctx->timing) { hipEventRecord(b, st); ctx->pending.push_back({name, a, b}); }
+}
+
+// bump carve of a device arena
+struct Carver {
+    uint8_t* base;
+    size_t off = 0;
+    explicit Carver(uint8_t* b) : base(b) {}
+    template <typename T> T* take(size_t count) {
+        off = (off + 255) & ~(size_t)255;
+        T* p = (T*)(base + off);
+        off += count * sizeof(T);
+        return p;
+    }
+};
+
+__global__ void iota_kernel(uint32_t* out, uint64_t n);
+
+int run_match_finder(Ctx* ctx, const Derived& d, const uint8_t* in, const uint64_t* d_offs, int nstreams,
+                     uint64_t total, bool wide_pairs, MfBuffers& w, hipStream_t st);
+
+struct EncArgs {
+    const uint8_t* in;            // padded batch copy
+    const uint64_t* offs;         // stream offsets (nstreams+1)
+    const uint32_t* order;        // processing order (longest first)
+    int nstreams;
+    unsigned int* next;           // work-queue counter
+    const uint32_t* minfo;
+    const void* pairs;
+    const uint32_t* ovf_off;
+    const void* ovf;
+    uint8_t* out;
+    const uint64_t* out_offs;     // capacity layout (nstreams+1)
+    uint64_t* out_lens;
+    int32_t* status;
+    uint8_t* scratch;             // per-block global scratch
+    uint64_t scratch_stride;
+    uint32_t fb, lc, lp, pb, eos, dist_table_size, len_table_size;
+    uint32_t lit_in_lds;
+};
+
+int launch_encoder(Ctx* ctx, const EncArgs& a, bool wide_pairs, int grid, hipStream_t st);
+uint32_t enc_lit_in_lds(const Derived& d);
+size_t enc_scratch_per_block(const Derived& d);
+
+struct DecArgs {
+    const uint8_t* in;
+    const uint64_t* in_offs;
+    const int64_t* out_sizes;
+    uint8_t* out;
+    const uint64_t* out_offs;
+    uint64_t* out_lens;
+    int32_t* status;
+    const uint32_t* order;
+    int nstreams;
+    unsigned int* next;
+    uint8_t* scratch;             // per-block literal probs when they do not fit LDS
+    uint64_t scratch_stride;
+    uint32_t lc, lp, pb, dict_check, lit_in_lds;
+};
+
+int launch_decoder(Ctx* ctx, const DecArgs& a, int grid, hipStream_t st);
+int dec_grid(uint32_t lc, uint32_t lp, uint32_t lit_in_lds, int nstreams);
+int enc_grid(const Derived& d, int nstreams);
+size_t enc_lds_bytes(const EncArgs& a);
+size_t dec_scratch_per_block(uint32_t lc, uint32_t lp);
+
+}  // namespace lzg
+
+struct lzma_ctx : lzg::Ctx {};

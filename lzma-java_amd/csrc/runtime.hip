@@ -1,0 +1,477 @@
+// runtime.hip -- host orchestration and the C ABI (include/lzma_mi355x.h).
+//
+// Encode of a batch of independent streams = one or more device passes, each
+// bounded by Ctx::batch_bytes of input:
+//   pad-copy input -> phase 1 match finder (mf.hip) -> phase 2 parser +
+//   range coder (enc.hip), all on one HIP stream; the host only reads back
+//   the per-stream lengths/status. Decode = dec.hip on the same model.
+// There is no CPU fallback: without a HIP device every entry point that
+// would compute returns LZMA_E_NODEVICE.
+#include <algorithm>
+#include <cstring>
+#include <numeric>
+#include <vector>
+
+#include "lzma_common.h"
+#include "runtime.h"
+
+namespace lzg {
+
+__global__ void iota_kernel(uint32_t* out, uint64_t n) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        out[i] = (uint32_t)i;
+}
+
+// gather per-stream outputs into a packed buffer: block per stream
+__global__ void pack_kernel(const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_offs,
+                            const uint64_t* __restrict__ dst_offs, uint8_t* __restrict__ dst, int nstreams) {
+    for (int s = blockIdx.x; s < nstreams; s += gridDim.x) {
+        uint64_t a = src_offs[s], o = dst_offs[s], len = dst_offs[s + 1] - o;
+        for (uint64_t i = threadIdx.x; i < len; i += blockDim.x) dst[o + i] = src[a + i];
+    }
+}
+
+static int check_device(Ctx* ctx) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0)
+        return ctx ? ctx->fail(LZMA_E_NODEVICE, "no HIP device (the MI355X path has no CPU fallback)") : LZMA_E_NODEVICE;
+    return LZMA_OK;
+}
+
+#define HIPCHK(x)                                                                      \
+    do {                                                                               \
+        hipError_t e_ = (x);                                                           \
+        if (e_ != hipSuccess) return ctx->fail(LZMA_E_DEVICE, "%s: %s", #x, hipGetErrorString(e_)); \
+    } while (0)
+
+// one encode pass over streams [s0, s1) of a batch
+static int encode_pass(Ctx* ctx, const Derived& d, const uint8_t* d_in, const uint64_t* h_offs, int s0, int s1,
+                       uint8_t* d_out, const uint64_t* h_out_offs, uint64_t* h_out_lens, int32_t* h_status,
+                       hipStream_t st) {
+    const int ns = s1 - s0;
+    const uint64_t in0 = h_offs[s0];
+    const uint64_t total = h_offs[s1] - in0;
+    bool wide = false;
+    std::vector<uint64_t> offs(ns + 1), oofs(ns + 1);
+    for (int i = 0; i <= ns; i++) { offs[i] = h_offs[s0 + i] - in0; oofs[i] = h_out_offs[s0 + i]; }
+    for (int i = 0; i < ns; i++)
+        if (offs[i + 1] - offs[i] >= PairPack<uint32_t>::kMaxStream) wide = true;
+    const size_t psz = wide ? 8 : 4;
+    // longest streams first (work queue order)
+    std::vector<uint32_t> order(ns);
+    std::iota(order.begin(), order.end(), 0u);
+    std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
+        return (offs[a + 1] - offs[a]) > (offs[b + 1] - offs[b]);
+    });
+    const int grid = enc_grid(d, ns);
+    const size_t scr = (enc_scratch_per_block(d) + 255) & ~(size_t)255;
+    uint64_t ovf_cap = total * std::max<uint64_t>(1, (d.fb + 2) / 16) + 65536;
+    if (ctx->ovf_hint > ovf_cap) ovf_cap = ctx->ovf_hint;
+    for (int attempt = 0; attempt < 6; attempt++) {
+        const uint64_t T = total;
+        auto need = [&](Carver& c, MfBuffers& w, uint8_t** inpad, uint64_t** d_offs, uint64_t** d_oofs,
+                        uint32_t** d_order, uint64_t** d_lens, int32_t** d_status, unsigned** d_next, uint8_t** d_scr) {
+            *inpad = c.take<uint8_t>(T + 512);
+            *d_offs = c.take<uint64_t>(ns + 1);
+            *d_oofs = c.take<uint64_t>(ns + 1);
+            *d_order = c.take<uint32_t>(ns);
+            *d_lens = c.take<uint64_t>(ns);
+            *d_status = c.take<int32_t>(ns);
+            *d_next = c.take<unsigned>(4);
+            w.k4 = c.take<uint64_t>(T); w.k3 = c.take<uint64_t>(T); w.k2 = c.take<uint64_t>(T); w.ks = c.take<uint64_t>(T);
+            w.vals = c.take<uint32_t>(T); w.vs = c.take<uint32_t>(T); w.minfo = c.take<uint32_t>(T);
+            w.prev2 = c.take<uint32_t>(T); w.prev3 = c.take<uint32_t>(T);
+            w.flag = c.take<uint8_t>(T);
+            w.chain_start = c.take<uint32_t>(T); w.chain_len = c.take<uint32_t>(T); w.chain_len_sorted = c.take<uint32_t>(T);
+            w.chain_idx = c.take<uint32_t>(T); w.chain_order = c.take<uint32_t>(T);
+            w.counts = c.take<uint64_t>(2);
+            w.son = c.take<uint32_t>(2 * T);
+            w.pairs = c.take<uint8_t>(T * kInlinePairs * psz);
+            w.ovf_off = c.take<uint32_t>(T);
+            w.ovf = c.take<uint8_t>(ovf_cap * psz);
+            w.ovf_cap = ovf_cap;
+            w.ovf_used = c.take<unsigned long long>(1);
+            w.err = c.take<int>(1);
+            *d_scr = c.take<uint8_t>((size_t)grid * scr);
+        };
+        MfBuffers w{};
+        uint8_t *inpad, *d_scr;
+        uint64_t *d_offs, *d_oofs, *d_lens;
+        uint32_t* d_order;
+        int32_t* d_status;
+        unsigned* d_next;
+        {
+            Carver probe(nullptr);
+            need(probe, w, &inpad, &d_offs, &d_oofs, &d_order, &d_lens, &d_status, &d_next, &d_scr);
+            if (!ctx->ensure_arena(probe.off + 4096)) return ctx->fail(LZMA_E_NOMEM, "device workspace %zu bytes", probe.off);
+        }
+        Carver c(ctx->arena);
+        need(c, w, &inpad, &d_offs, &d_oofs, &d_order, &d_lens, &d_status, &d_next, &d_scr);
+        {
+            TimedLaunch tl(ctx, "enc_stage", st);
+            HIPCHK(hipMemcpyAsync(inpad, d_in + in0, total, hipMemcpyDeviceToDevice, st));
+            HIPCHK(hipMemsetAsync(inpad + total, 0, 512, st));
+            HIPCHK(hipMemcpyAsync(d_offs, offs.data(), (ns + 1) * 8, hipMemcpyHostToDevice, st));
+            HIPCHK(hipMemcpyAsync(d_oofs, oofs.data(), (ns + 1) * 8, hipMemcpyHostToDevice, st));
+            HIPCHK(hipMemcpyAsync(d_order, order.data(), ns * 4, hipMemcpyHostToDevice, st));
+            HIPCHK(hipMemsetAsync(d_next, 0, 16, st));
+        }
+        int rc = run_match_finder(ctx, d, inpad, d_offs, ns, total, wide, w, st);
+        if (rc == LZMA_E_OVERFLOW) {
+            ovf_cap *= 4;
+            ctx->ovf_hint = ovf_cap;
+            continue;
+        }
+        if (rc) return rc;
+        EncArgs a{};
+        a.in = inpad; a.offs = d_offs; a.order = d_order; a.nstreams = ns; a.next = d_next;
+        a.minfo = w.minfo; a.pairs = w.pairs; a.ovf_off = w.ovf_off; a.ovf = w.ovf;
+        a.out = d_out; a.out_offs = d_oofs; a.out_lens = d_lens; a.status = d_status;
+        a.scratch = d_scr; a.scratch_stride = scr;
+        a.fb = d.fb; a.lc = d.lc; a.lp = d.lp; a.pb = d.pb; a.eos = d.eos;
+        a.dist_table_size = d.dist_table_size; a.len_table_size = d.len_table_size;
+        a.lit_in_lds = enc_lit_in_lds(d);
+        if ((rc = launch_encoder(ctx, a, wide, grid, st))) return rc;
+        HIPCHK(hipMemcpyAsync(h_out_lens + s0, d_lens, ns * 8, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipMemcpyAsync(h_status + s0, d_status, ns * 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        return LZMA_OK;
+    }
+    return ctx->fail(LZMA_E_NOMEM, "match-pair overflow pool kept overflowing");
+}
+
+static int encode_batch_dev(Ctx* ctx, const lzma_params* p, const uint8_t* d_in, const uint64_t* h_offs, int nstreams,
+                            uint8_t* d_out, const uint64_t* h_out_offs, uint64_t* h_out_lens, hipStream_t st) {
+    Derived d;
+    if (derive(*p, d) != LZMA_OK) return ctx->fail(LZMA_E_PARAM, "invalid lzma_params");
+    if (nstreams < 0) return ctx->fail(LZMA_E_PARAM, "nstreams < 0");
+    if (nstreams == 0) return LZMA_OK;
+    for (int i = 0; i < nstreams; i++) {
+        if (h_offs[i + 1] < h_offs[i] || h_out_offs[i + 1] < h_out_offs[i]) return ctx->fail(LZMA_E_PARAM, "offsets not monotone");
+        if (h_offs[i + 1] - h_offs[i] >= (1ull << 31)) return ctx->fail(LZMA_E_PARAM, "stream %d >= 2 GiB", i);
+    }
+    std::vector<int32_t> status(nstreams, 0);
+    int s0 = 0;
+    while (s0 < nstreams) {
+        int s1 = s0 + 1;
+        while (s1 < nstreams && h_offs[s1 + 1] - h_offs[s0] <= ctx->batch_bytes) s1++;
+        int rc = encode_pass(ctx, d, d_in, h_offs, s0, s1, d_out, h_out_offs, h_out_lens, status.data(), st);
+        if (rc) return rc;
+        s0 = s1;
+    }
+    for (int i = 0; i < nstreams; i++)
+        if (status[i] != LZMA_OK) return ctx->fail(status[i], "stream %d: output capacity too small", i);
+    return LZMA_OK;
+}
+
+static int decode_batch_dev(Ctx* ctx, const uint8_t props[5], const uint8_t* d_in, const uint64_t* h_in_offs, int nstreams,
+                            const int64_t* h_out_sizes, uint8_t* d_out, const uint64_t* h_out_offs, uint64_t* h_out_lens,
+                            int32_t* h_status, hipStream_t st) {
+    lzma_params p;
+    if (lzma_read_props(props, &p) != LZMA_OK) return ctx->fail(LZMA_E_PARAM, "bad properties (Decoder.SetDecoderProperties false)");
+    if (nstreams <= 0) return nstreams == 0 ? LZMA_OK : ctx->fail(LZMA_E_PARAM, "nstreams < 0");
+    uint32_t dict = (uint32_t)props[1] | ((uint32_t)props[2] << 8) | ((uint32_t)props[3] << 16) | ((uint32_t)props[4] << 24);
+    const uint32_t lc = (uint32_t)p.lc, lp = (uint32_t)p.lp, pb = (uint32_t)p.pb;
+    const uint32_t lit_lds = (lc + lp) <= 3;
+    std::vector<uint32_t> order(nstreams);
+    std::iota(order.begin(), order.end(), 0u);
+    std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
+        return (h_out_offs[a + 1] - h_out_offs[a]) > (h_out_offs[b + 1] - h_out_offs[b]);
+    });
+    const int grid = dec_grid(lc, lp, lit_lds, nstreams);
+    const size_t scr = lit_lds ? 0 : ((dec_scratch_per_block(lc, lp) + 255) & ~(size_t)255);
+    Carver probe(nullptr);
+    probe.take<uint64_t>(nstreams + 1); probe.take<int64_t>(nstreams); probe.take<uint64_t>(nstreams + 1);
+    probe.take<uint64_t>(nstreams); probe.take<int32_t>(nstreams); probe.take<uint32_t>(nstreams);
+    probe.take<unsigned>(4); probe.take<uint8_t>((size_t)grid * scr + 16);
+    if (!ctx->ensure_arena(probe.off + 4096)) return ctx->fail(LZMA_E_NOMEM, "decoder workspace");
+    Carver c(ctx->arena);
+    uint64_t* d_in_offs = c.take<uint64_t>(nstreams + 1);
+    int64_t* d_sizes = c.take<int64_t>(nstreams);
+    uint64_t* d_oofs = c.take<uint64_t>(nstreams + 1);
+    uint64_t* d_lens = c.take<uint64_t>(nstreams);
+    int32_t* d_status = c.take<int32_t>(nstreams);
+    uint32_t* d_order = c.take<uint32_t>(nstreams);
+    unsigned* d_next = c.take<unsigned>(4);
+    uint8_t* d_scr = c.take<uint8_t>((size_t)grid * scr + 16);
+    HIPCHK(hipMemcpyAsync(d_in_offs, h_in_offs, (nstreams + 1) * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(d_sizes, h_out_sizes, nstreams * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(d_oofs, h_out_offs, (nstreams + 1) * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(d_order, order.data(), nstreams * 4, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemsetAsync(d_next, 0, 16, st));
+    DecArgs a{};
+    a.in = d_in; a.in_offs = d_in_offs; a.out_sizes = d_sizes; a.out = d_out; a.out_offs = d_oofs;
+    a.out_lens = d_lens; a.status = d_status; a.order = d_order; a.nstreams = nstreams; a.next = d_next;
+    a.scratch = d_scr; a.scratch_stride = scr; a.lc = lc; a.lp = lp; a.pb = pb;
+    a.dict_check = dict > 1 ? dict : 1;
+    a.lit_in_lds = lit_lds;
+    int rc = launch_decoder(ctx, a, grid, st);
+    if (rc) return rc;
+    HIPCHK(hipMemcpyAsync(h_out_lens, d_lens, nstreams * 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(h_status, d_status, nstreams * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    return LZMA_OK;
+}
+
+}  // namespace lzg
+
+using namespace lzg;
+
+extern "C" {
+
+const char* lzma_version(void) { return "lzma-mi355x 0.1 (gfx950)"; }
+
+int lzma_params_default(lzma_params* p) {   // Encoder field defaults, Encoder.java:135-172
+    if (!p) return LZMA_E_PARAM;
+    p->dict_size = 1 << 22;
+    p->fb = 32;
+    p->mf = 1;
+    p->lc = 3;
+    p->lp = 0;
+    p->pb = 2;
+    p->eos = 0;
+    return LZMA_OK;
+}
+
+int lzma_params_check(const lzma_params* p) {
+    if (!p) return LZMA_E_PARAM;
+    Derived d;
+    return derive(*p, d);
+}
+
+int lzma_write_props(const lzma_params* p, uint8_t out[5]) {   // Encoder.java:1079-1085
+    if (!p || !out) return LZMA_E_PARAM;
+    out[0] = (uint8_t)((p->pb * 5 + p->lp) * 9 + p->lc);
+    for (int i = 0; i < 4; i++) out[1 + i] = (uint8_t)((uint32_t)p->dict_size >> (8 * i));
+    return LZMA_OK;
+}
+
+int lzma_read_props(const uint8_t in[5], lzma_params* p) {   // Decoder.java:303-318
+    if (!in || !p) return LZMA_E_PARAM;
+    uint32_t v = in[0];
+    int lc = (int)(v % 9), rem = (int)(v / 9), lp = rem % 5, pb = rem / 5;
+    int32_t dict = (int32_t)((uint32_t)in[1] | ((uint32_t)in[2] << 8) | ((uint32_t)in[3] << 16) | ((uint32_t)in[4] << 24));
+    if (lc > 8 || lp > 4 || pb > 4) return LZMA_E_PARAM;   // SetLcLpPb :172-182
+    if (dict < 0) return LZMA_E_PARAM;                      // SetDictionarySize :160-170
+    p->lc = lc; p->lp = lp; p->pb = pb; p->dict_size = dict;
+    p->fb = 32; p->mf = 1; p->eos = 0;
+    return LZMA_OK;
+}
+
+uint64_t lzma_enc_bound(uint64_t n) { return n + n / 8 + 4096; }
+
+int lzma_ctx_create(int device, lzma_ctx** out) {
+    if (!out) return LZMA_E_PARAM;
+    *out = nullptr;
+    int rc = check_device(nullptr);
+    if (rc) return rc;
+    if (hipSetDevice(device) != hipSuccess) return LZMA_E_DEVICE;
+    lzma_ctx* c = new lzma_ctx();
+    c->device = device;
+    *out = c;
+    return LZMA_OK;
+}
+
+void lzma_ctx_destroy(lzma_ctx* ctx) {
+    if (!ctx) return;
+    hipSetDevice(ctx->device);
+    ctx->resolve_timings();
+    for (auto e : ctx->free_events) hipEventDestroy(e);
+    if (ctx->arena) hipFree(ctx->arena);
+    if (ctx->tmp) hipFree(ctx->tmp);
+    delete ctx;
+}
+
+const char* lzma_last_error(const lzma_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int lzma_ctx_set_batch_bytes(lzma_ctx* ctx, uint64_t bytes) {
+    if (!ctx || bytes < 4096) return LZMA_E_PARAM;
+    ctx->batch_bytes = bytes;
+    return LZMA_OK;
+}
+
+int lzma_ctx_set_timing(lzma_ctx* ctx, int on) {
+    if (!ctx) return LZMA_E_PARAM;
+    ctx->timing = on != 0;
+    return LZMA_OK;
+}
+
+int lzma_ctx_timings(lzma_ctx* ctx, const char** names, double* ms, int64_t* launches, int cap) {
+    if (!ctx) return LZMA_E_PARAM;
+    hipSetDevice(ctx->device);
+    ctx->resolve_timings();
+    int i = 0;
+    for (auto& kv : ctx->acc) {
+        if (i >= cap) break;
+        if (names) names[i] = kv.first.c_str();
+        if (ms) ms[i] = kv.second.ms;
+        if (launches) launches[i] = kv.second.n;
+        i++;
+    }
+    return i;
+}
+
+void lzma_ctx_reset_timings(lzma_ctx* ctx) {
+    if (!ctx) return;
+    ctx->resolve_timings();
+    ctx->acc.clear();
+}
+
+int lzma_enc_batch_dev(lzma_ctx* ctx, const lzma_params* p, const uint8_t* d_in, const uint64_t* h_offs, int nstreams,
+                       uint8_t* d_out, const uint64_t* h_out_offs, uint64_t* h_out_lens, void* hip_stream) {
+    if (!ctx || !p || !h_offs || !h_out_offs || !h_out_lens) return LZMA_E_PARAM;
+    if (check_device(ctx)) return LZMA_E_NODEVICE;
+    hipSetDevice(ctx->device);
+    return encode_batch_dev(ctx, p, d_in, h_offs, nstreams, d_out, h_out_offs, h_out_lens, (hipStream_t)hip_stream);
+}
+
+int lzma_enc_batch(lzma_ctx* ctx, const lzma_params* p, const uint8_t* in, const uint64_t* offs, int nstreams,
+                   uint8_t* out, uint64_t out_cap, uint64_t* out_offs) {
+    if (!ctx || !p || !offs || !out_offs || nstreams < 0) return LZMA_E_PARAM;
+    if (check_device(ctx)) return LZMA_E_NODEVICE;
+    hipSetDevice(ctx->device);
+    Derived d;
+    if (derive(*p, d) != LZMA_OK) return ctx->fail(LZMA_E_PARAM, "invalid lzma_params");
+    const uint64_t total = offs[nstreams] - offs[0];
+    std::vector<uint64_t> rel(nstreams + 1), cap_offs(nstreams + 1), lens(nstreams);
+    cap_offs[0] = 0;
+    for (int i = 0; i <= nstreams; i++) rel[i] = offs[i] - offs[0];
+    for (int i = 0; i < nstreams; i++) cap_offs[i + 1] = cap_offs[i] + lzma_enc_bound(rel[i + 1] - rel[i]);
+    uint8_t *d_in = nullptr, *d_out = nullptr, *d_pack = nullptr;
+    uint64_t *d_co = nullptr, *d_po = nullptr;
+    int rc = LZMA_OK;
+    std::vector<uint64_t> pack(nstreams + 1);
+    hipStream_t st = nullptr;
+    if (hipMalloc(&d_in, total + 1) != hipSuccess || hipMalloc(&d_out, cap_offs[nstreams] + 1) != hipSuccess) {
+        rc = ctx->fail(LZMA_E_NOMEM, "device buffers");
+        goto done;
+    }
+    if (total && hipMemcpy(d_in, in + offs[0], total, hipMemcpyHostToDevice) != hipSuccess) { rc = ctx->fail(LZMA_E_DEVICE, "H2D"); goto done; }
+    rc = encode_batch_dev(ctx, p, d_in, rel.data(), nstreams, d_out, cap_offs.data(), lens.data(), st);
+    if (rc) goto done;
+    pack[0] = 0;
+    for (int i = 0; i < nstreams; i++) pack[i + 1] = pack[i] + lens[i];
+    if (pack[nstreams] > out_cap) { rc = ctx->fail(LZMA_E_OVERFLOW, "out_cap %llu < %llu", (unsigned long long)out_cap, (unsigned long long)pack[nstreams]); goto done; }
+    if (hipMalloc(&d_pack, pack[nstreams] + 1) != hipSuccess || hipMalloc(&d_co, (nstreams + 1) * 8) != hipSuccess ||
+        hipMalloc(&d_po, (nstreams + 1) * 8) != hipSuccess) { rc = ctx->fail(LZMA_E_NOMEM, "pack buffers"); goto done; }
+    hipMemcpy(d_co, cap_offs.data(), (nstreams + 1) * 8, hipMemcpyHostToDevice);
+    hipMemcpy(d_po, pack.data(), (nstreams + 1) * 8, hipMemcpyHostToDevice);
+    if (nstreams > 0) hipLaunchKernelGGL(pack_kernel, dim3(std::min(nstreams, 65535)), dim3(256), 0, st, d_out, d_co, d_po, d_pack, nstreams);
+    if (pack[nstreams] && hipMemcpy(out, d_pack, pack[nstreams], hipMemcpyDeviceToHost) != hipSuccess) { rc = ctx->fail(LZMA_E_DEVICE, "D2H"); goto done; }
+    for (int i = 0; i <= nstreams; i++) out_offs[i] = pack[i];
+done:
+    hipFree(d_in); hipFree(d_out); hipFree(d_pack); hipFree(d_co); hipFree(d_po);
+    return rc;
+}
+
+int lzma_encode(lzma_ctx* ctx, const lzma_params* p, const uint8_t* in, uint64_t n, uint8_t* out, uint64_t out_cap,
+                uint64_t* out_len) {
+    uint64_t offs[2] = {0, n}, oo[2] = {0, 0};
+    int rc = lzma_enc_batch(ctx, p, in, offs, 1, out, out_cap, oo);
+    if (rc == LZMA_OK && out_len) *out_len = oo[1];
+    return rc;
+}
+
+int lzma_dec_batch_dev(lzma_ctx* ctx, const uint8_t props[5], const uint8_t* d_in, const uint64_t* h_in_offs, int nstreams,
+                       const int64_t* h_out_sizes, uint8_t* d_out, const uint64_t* h_out_offs, uint64_t* h_out_lens,
+                       int32_t* h_status, void* hip_stream) {
+    if (!ctx || !props || !h_in_offs || !h_out_sizes || !h_out_offs || !h_out_lens || !h_status) return LZMA_E_PARAM;
+    if (check_device(ctx)) return LZMA_E_NODEVICE;
+    hipSetDevice(ctx->device);
+    return decode_batch_dev(ctx, props, d_in, h_in_offs, nstreams, h_out_sizes, d_out, h_out_offs, h_out_lens, h_status,
+                            (hipStream_t)hip_stream);
+}
+
+int lzma_dec_batch(lzma_ctx* ctx, const uint8_t props[5], const uint8_t* in, const uint64_t* in_offs, int nstreams,
+                   const int64_t* out_sizes, uint8_t* out, const uint64_t* out_offs, uint64_t* out_lens, int32_t* status) {
+    if (!ctx || !props || !in_offs || !out_sizes || !out_offs || !out_lens || !status || nstreams < 0) return LZMA_E_PARAM;
+    if (check_device(ctx)) return LZMA_E_NODEVICE;
+    hipSetDevice(ctx->device);
+    const uint64_t tin = in_offs[nstreams] - in_offs[0];
+    const uint64_t tout = out_offs[nstreams] - out_offs[0];
+    std::vector<uint64_t> rin(nstreams + 1), rout(nstreams + 1);
+    for (int i = 0; i <= nstreams; i++) { rin[i] = in_offs[i] - in_offs[0]; rout[i] = out_offs[i] - out_offs[0]; }
+    uint8_t *d_in = nullptr, *d_out = nullptr;
+    int rc = LZMA_OK;
+    if (hipMalloc(&d_in, tin + 1) != hipSuccess || hipMalloc(&d_out, tout + 1) != hipSuccess) {
+        rc = ctx->fail(LZMA_E_NOMEM, "device buffers");
+    } else {
+        if (tin) hipMemcpy(d_in, in + in_offs[0], tin, hipMemcpyHostToDevice);
+        rc = decode_batch_dev(ctx, props, d_in, rin.data(), nstreams, out_sizes, d_out, rout.data(), out_lens, status, nullptr);
+        if (rc == LZMA_OK && tout) {
+            for (int i = 0; i < nstreams; i++) {
+                uint64_t L = std::min<uint64_t>(out_lens[i], rout[i + 1] - rout[i]);
+                if (L) hipMemcpy(out + out_offs[i], d_out + rout[i], L, hipMemcpyDeviceToHost);
+            }
+        }
+    }
+    hipFree(d_in);
+    hipFree(d_out);
+    return rc;
+}
+
+int lzma_decode(lzma_ctx* ctx, const uint8_t props[5], const uint8_t* in, uint64_t n, int64_t out_size, uint8_t* out,
+                uint64_t out_cap, uint64_t* out_len) {
+    uint64_t io[2] = {0, n}, oo[2] = {0, out_cap}, len = 0;
+    int32_t st = 0;
+    int rc = lzma_dec_batch(ctx, props, in, io, 1, &out_size, out, oo, &len, &st);
+    if (out_len) *out_len = len;
+    if (rc) return rc;
+    return st;
+}
+
+// LzmaBench.CBenchRandomGenerator (LzmaBench.java:15-127): MWC RNG, bit
+// reservoir, literal with p = 1/2 else a short-offset copy.
+void lzma_bench_generate(uint8_t* buf, uint64_t size) {
+    uint32_t A1 = 362436069u, A2 = 521288629u;   // CRandomGenerator.Init :23-26
+    uint32_t value = 0;
+    int num_bits = 0;
+    auto rnd32 = [&]() -> uint32_t {   // GetRnd :28-32
+        A1 = 36969u * (A1 & 0xffffu) + (A1 >> 16);
+        A2 = 18000u * (A2 & 0xffffu) + (A2 >> 16);
+        return (A1 << 16) ^ A2;
+    };
+    auto get = [&](int nb) -> uint32_t {   // CBitRandomGenerator.GetRnd :45-60
+        uint32_t result;
+        if (num_bits > nb) {
+            result = value & ((1u << nb) - 1);
+            value >>= nb;
+            num_bits -= nb;
+            return result;
+        }
+        nb -= num_bits;
+        result = nb >= 32 ? 0 : (value << nb);
+        value = rnd32();
+        result |= value & (nb >= 32 ? 0xFFFFFFFFu : ((1u << nb) - 1));
+        value = nb >= 32 ? 0 : (value >> nb);
+        num_bits = 32 - nb;
+        return result;
+    };
+    auto log_bits = [&](int nb) -> uint32_t { uint32_t len = get(nb); return get((int)len); };   // :84-87
+    uint64_t pos = 0;
+    uint32_t rep0 = 1;
+    while (pos < size) {   // Generate :104-127
+        if (get(1) == 0 || pos < 1) {
+            buf[pos++] = (uint8_t)get(8);
+        } else {
+            uint32_t len;
+            if (get(3) == 0) {
+                len = 1 + get(1 + (int)get(2));
+            } else {
+                do {
+                    if (get(1) == 0) {
+                        rep0 = log_bits(4);
+                    } else {   // Java evaluates left to right: high part first
+                        uint32_t hi = log_bits(4);
+                        rep0 = (hi << 10) | get(10);
+                    }
+                } while (rep0 >= pos);
+                rep0++;
+                len = 2 + get(2 + (int)get(2));
+            }
+            for (uint32_t i = 0; i < len && pos < size; i++, pos++) buf[pos] = buf[pos - rep0];
+        }
+    }
+}
+
+}  // extern "C"

@@ -1,0 +1,400 @@
+"""lzma_amd -- MI355X-native drop-in for the rfalke/lzma-java LZMA hot path.
+
+Host-side mirror of the reference's codec API, over the C ABI in
+include/lzma_mi355x.h (built as lzma-java_amd/build/liblzma_mi355x.so):
+
+  Encoder   <- SevenZip.Compression.LZMA.Encoder  (Encoder.java:16)
+  Decoder   <- SevenZip.Compression.LZMA.Decoder  (Decoder.java:12)
+
+Same method names, argument meaning and error behaviour as the Java classes:
+setters return False on out-of-range values, Encoder.Code writes the raw
+range-coder stream (the caller writes the .lzma header, LzmaAlone.java:
+208-217), Decoder.Code returns False on corrupt data. All coding runs on the
+GPU; there is no CPU fallback -- without the built library or a HIP device
+every coding call raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_PKG = os.path.dirname(_HERE)
+LIB_PATH = os.path.join(_PKG, "build", "liblzma_mi355x.so")
+
+LZMA_OK = 0
+LZMA_E_PARAM = -1
+LZMA_E_NOMEM = -2
+LZMA_E_DEVICE = -3
+LZMA_E_OVERFLOW = -4
+LZMA_E_DATA = -5
+LZMA_E_NODEVICE = -6
+LZMA_E_INTERNAL = -7
+
+EXPORTED_SYMBOLS = [
+    "lzma_version", "lzma_params_default", "lzma_params_check", "lzma_write_props", "lzma_read_props",
+    "lzma_enc_bound", "lzma_ctx_create", "lzma_ctx_destroy", "lzma_last_error", "lzma_ctx_set_batch_bytes",
+    "lzma_ctx_set_timing", "lzma_ctx_timings", "lzma_ctx_reset_timings", "lzma_enc_batch_dev", "lzma_enc_batch",
+    "lzma_encode", "lzma_dec_batch_dev", "lzma_dec_batch", "lzma_decode", "lzma_bench_generate",
+]
+
+
+class LzmaError(RuntimeError):
+    def __init__(self, code, msg=""):
+        super().__init__("lzma error %d: %s" % (code, msg))
+        self.code = code
+
+
+class Params(ctypes.Structure):
+    _fields_ = [("dict_size", ctypes.c_int32), ("fb", ctypes.c_int32), ("mf", ctypes.c_int32),
+                ("lc", ctypes.c_int32), ("lp", ctypes.c_int32), ("pb", ctypes.c_int32), ("eos", ctypes.c_int32)]
+
+    def __repr__(self):
+        return "Params(dict_size=%d, fb=%d, mf=%d, lc=%d, lp=%d, pb=%d, eos=%d)" % (
+            self.dict_size, self.fb, self.mf, self.lc, self.lp, self.pb, self.eos)
+
+
+_lib_handle = None
+
+
+def lib():
+    """Load the product library; raises if it was not built (no fallback)."""
+    global _lib_handle
+    if _lib_handle is None:
+        if not os.path.exists(LIB_PATH):
+            raise LzmaError(LZMA_E_INTERNAL, "%s not built (run `make -C lzma-java_amd` or "
+                                             "__graft_entry__.build())" % LIB_PATH)
+        L = ctypes.CDLL(LIB_PATH)
+        vp, u64, i32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int
+        P = ctypes.POINTER(Params)
+        L.lzma_version.restype = ctypes.c_char_p
+        L.lzma_params_default.argtypes = [P]
+        L.lzma_params_check.argtypes = [P]
+        L.lzma_write_props.argtypes = [P, vp]
+        L.lzma_read_props.argtypes = [vp, P]
+        L.lzma_enc_bound.argtypes = [u64]
+        L.lzma_enc_bound.restype = u64
+        L.lzma_ctx_create.argtypes = [i32, ctypes.POINTER(vp)]
+        L.lzma_ctx_destroy.argtypes = [vp]
+        L.lzma_last_error.argtypes = [vp]
+        L.lzma_last_error.restype = ctypes.c_char_p
+        L.lzma_ctx_set_batch_bytes.argtypes = [vp, u64]
+        L.lzma_ctx_set_timing.argtypes = [vp, i32]
+        L.lzma_ctx_timings.argtypes = [vp, vp, vp, vp, i32]
+        L.lzma_ctx_reset_timings.argtypes = [vp]
+        L.lzma_enc_batch_dev.argtypes = [vp, P, vp, vp, i32, vp, vp, vp, vp]
+        L.lzma_enc_batch.argtypes = [vp, P, vp, vp, i32, vp, u64, vp]
+        L.lzma_encode.argtypes = [vp, P, vp, u64, vp, u64, ctypes.POINTER(u64)]
+        L.lzma_dec_batch_dev.argtypes = [vp, vp, vp, vp, i32, vp, vp, vp, vp, vp, vp]
+        L.lzma_dec_batch.argtypes = [vp, vp, vp, vp, i32, vp, vp, vp, vp, vp]
+        L.lzma_decode.argtypes = [vp, vp, vp, u64, ctypes.c_int64, vp, u64, ctypes.POINTER(u64)]
+        L.lzma_bench_generate.argtypes = [vp, u64]
+        L.lzma_bench_generate.restype = None
+        _lib_handle = L
+    return _lib_handle
+
+
+def version() -> str:
+    return lib().lzma_version().decode()
+
+
+def default_params() -> Params:
+    p = Params()
+    lib().lzma_params_default(ctypes.byref(p))
+    return p
+
+
+def make_params(dict_size=1 << 22, fb=32, mf=1, lc=3, lp=0, pb=2, eos=False) -> Params:
+    return Params(int(dict_size), int(fb), int(mf), int(lc), int(lp), int(pb), 1 if eos else 0)
+
+
+def params_ok(p: Params) -> bool:
+    return lib().lzma_params_check(ctypes.byref(p)) == LZMA_OK
+
+
+def write_props(p: Params) -> bytes:
+    b = (ctypes.c_uint8 * 5)()
+    lib().lzma_write_props(ctypes.byref(p), b)
+    return bytes(b)
+
+
+def read_props(props: bytes) -> Optional[Params]:
+    p = Params()
+    b = (ctypes.c_uint8 * 5)(*props[:5])
+    return p if lib().lzma_read_props(b, ctypes.byref(p)) == LZMA_OK else None
+
+
+def enc_bound(n: int) -> int:
+    return int(lib().lzma_enc_bound(n))
+
+
+def bench_generate(size: int) -> np.ndarray:
+    """LzmaBench.CBenchRandomGenerator output (LzmaBench.java:104-127)."""
+    buf = np.empty(max(size, 1), dtype=np.uint8)
+    lib().lzma_bench_generate(buf.ctypes.data, size)
+    return buf[:size]
+
+
+class Context:
+    """One HIP device plus its device workspace (lzma_ctx)."""
+
+    def __init__(self, device: int = 0):
+        h = ctypes.c_void_p()
+        rc = lib().lzma_ctx_create(device, ctypes.byref(h))
+        if rc != LZMA_OK:
+            raise LzmaError(rc, "lzma_ctx_create(device=%d) failed%s" % (
+                device, " (no HIP device; the MI355X path has no CPU fallback)" if rc == LZMA_E_NODEVICE else ""))
+        self.h = h
+        self.device = device
+
+    def close(self):
+        if self.h:
+            lib().lzma_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def error(self) -> str:
+        return lib().lzma_last_error(self.h).decode()
+
+    def check(self, rc):
+        if rc != LZMA_OK:
+            raise LzmaError(rc, self.error())
+
+    def set_batch_bytes(self, n: int):
+        self.check(lib().lzma_ctx_set_batch_bytes(self.h, n))
+
+    def set_timing(self, on: bool):
+        self.check(lib().lzma_ctx_set_timing(self.h, 1 if on else 0))
+
+    def timings(self) -> dict:
+        cap = 32
+        names = (ctypes.c_char_p * cap)()
+        ms = (ctypes.c_double * cap)()
+        n = (ctypes.c_int64 * cap)()
+        k = lib().lzma_ctx_timings(self.h, names, ms, n, cap)
+        return {names[i].decode(): (ms[i], n[i]) for i in range(k)}
+
+    def reset_timings(self):
+        lib().lzma_ctx_reset_timings(self.h)
+
+    # ---- host-buffer batch API
+    def encode_batch(self, streams: Sequence[bytes], p: Params) -> List[bytes]:
+        arrs = [np.frombuffer(s, dtype=np.uint8) if not isinstance(s, np.ndarray) else s for s in streams]
+        offs = np.zeros(len(arrs) + 1, dtype=np.uint64)
+        np.cumsum([a.size for a in arrs], out=offs[1:])
+        data = np.concatenate(arrs) if arrs and offs[-1] > 0 else np.zeros(1, dtype=np.uint8)
+        cap = int(sum(enc_bound(a.size) for a in arrs)) + 1
+        out = np.empty(cap, dtype=np.uint8)
+        oo = np.zeros(len(arrs) + 1, dtype=np.uint64)
+        self.check(lib().lzma_enc_batch(self.h, ctypes.byref(p), data.ctypes.data, offs.ctypes.data, len(arrs),
+                                        out.ctypes.data, cap, oo.ctypes.data))
+        return [out[oo[i]:oo[i + 1]].tobytes() for i in range(len(arrs))]
+
+    def decode_batch(self, streams: Sequence[bytes], props: bytes, out_sizes: Sequence[int],
+                     caps: Optional[Sequence[int]] = None) -> List[Tuple[int, bytes]]:
+        arrs = [np.frombuffer(s, dtype=np.uint8) for s in streams]
+        n = len(arrs)
+        io = np.zeros(n + 1, dtype=np.uint64)
+        np.cumsum([a.size for a in arrs], out=io[1:])
+        data = np.concatenate(arrs) if n and io[-1] > 0 else np.zeros(1, dtype=np.uint8)
+        if caps is None:
+            caps = [s if s >= 0 else max(64 * a.size, 4096) for s, a in zip(out_sizes, arrs)]
+        oo = np.zeros(n + 1, dtype=np.uint64)
+        np.cumsum(caps, out=oo[1:])
+        out = np.zeros(int(oo[-1]) + 1, dtype=np.uint8)
+        sizes = np.array(out_sizes, dtype=np.int64)
+        lens = np.zeros(n, dtype=np.uint64)
+        status = np.zeros(n, dtype=np.int32)
+        self.check(lib().lzma_dec_batch(self.h, (ctypes.c_uint8 * 5)(*props[:5]), data.ctypes.data, io.ctypes.data, n,
+                                        sizes.ctypes.data, out.ctypes.data, oo.ctypes.data, lens.ctypes.data,
+                                        status.ctypes.data))
+        res = []
+        for i in range(n):
+            L = min(int(lens[i]), int(oo[i + 1] - oo[i]))
+            res.append((int(status[i]), out[oo[i]:oo[i] + L].tobytes()))
+        return res
+
+    # ---- device-resident batch API (torch tensors already in HBM)
+    def encode_batch_dev(self, d_in, offs: np.ndarray, p: Params, d_out, out_offs: np.ndarray, stream_ptr: int = 0):
+        """d_in/d_out: device pointers (int) or torch uint8 cuda tensors."""
+        n = len(offs) - 1
+        lens = np.zeros(max(n, 1), dtype=np.uint64)
+        offs = np.ascontiguousarray(offs, dtype=np.uint64)
+        out_offs = np.ascontiguousarray(out_offs, dtype=np.uint64)
+        self.check(lib().lzma_enc_batch_dev(self.h, ctypes.byref(p), _dptr(d_in), offs.ctypes.data, n, _dptr(d_out),
+                                            out_offs.ctypes.data, lens.ctypes.data, ctypes.c_void_p(stream_ptr)))
+        return lens[:n]
+
+    def decode_batch_dev(self, props: bytes, d_in, in_offs: np.ndarray, out_sizes: np.ndarray, d_out,
+                         out_offs: np.ndarray, stream_ptr: int = 0):
+        n = len(in_offs) - 1
+        in_offs = np.ascontiguousarray(in_offs, dtype=np.uint64)
+        out_offs = np.ascontiguousarray(out_offs, dtype=np.uint64)
+        sizes = np.ascontiguousarray(out_sizes, dtype=np.int64)
+        lens = np.zeros(max(n, 1), dtype=np.uint64)
+        status = np.zeros(max(n, 1), dtype=np.int32)
+        self.check(lib().lzma_dec_batch_dev(self.h, (ctypes.c_uint8 * 5)(*props[:5]), _dptr(d_in), in_offs.ctypes.data,
+                                            n, sizes.ctypes.data, _dptr(d_out), out_offs.ctypes.data,
+                                            lens.ctypes.data, status.ctypes.data, ctypes.c_void_p(stream_ptr)))
+        return lens[:n], status[:n]
+
+
+def _dptr(x) -> ctypes.c_void_p:
+    if hasattr(x, "data_ptr"):
+        return ctypes.c_void_p(x.data_ptr())
+    return ctypes.c_void_p(int(x))
+
+
+_default_ctx = None
+
+
+def default_context() -> Context:
+    global _default_ctx
+    if _default_ctx is None:
+        _default_ctx = Context(0)
+    return _default_ctx
+
+
+# --------------------------------------------------------------------------
+# Drop-in mirrors of the Java classes
+# --------------------------------------------------------------------------
+
+def _read_all(stream) -> bytes:
+    if isinstance(stream, (bytes, bytearray, memoryview)):
+        return bytes(stream)
+    chunks = []
+    while True:
+        b = stream.read(1 << 20)
+        if not b:
+            break
+        chunks.append(b)
+    return b"".join(chunks)
+
+
+class Encoder:
+    """Mirror of SevenZip.Compression.LZMA.Encoder (Encoder.java:16-1185)."""
+
+    EMatchFinderTypeBT2 = 0
+    EMatchFinderTypeBT4 = 1
+    kDefaultDictionaryLogSize = 22
+    kNumFastBytesDefault = 0x20
+
+    def __init__(self, ctx: Optional[Context] = None):
+        self._ctx = ctx
+        self._p = make_params()
+        self._p.dict_size = 1 << self.kDefaultDictionaryLogSize
+        self._p.fb = self.kNumFastBytesDefault
+
+    @staticmethod
+    def SetAlgorithm(algorithm: int) -> bool:   # Encoder.java:1127-1133 (a no-op in the reference)
+        return True
+
+    def SetDictionarySize(self, dictionarySize: int) -> bool:   # :1135-1146
+        if dictionarySize < 1 or dictionarySize > (1 << 29):
+            return False
+        self._p.dict_size = dictionarySize
+        return True
+
+    def SetNumFastBytes(self, numFastBytes: int) -> bool:   # :1148-1154
+        if numFastBytes < 5 or numFastBytes > 273:
+            return False
+        self._p.fb = numFastBytes
+        return True
+
+    def SetMatchFinder(self, matchFinderIndex: int) -> bool:   # :1156-1167
+        if matchFinderIndex < 0 or matchFinderIndex > 2:
+            return False
+        self._p.mf = matchFinderIndex
+        return True
+
+    def SetLcLpPb(self, lc: int, lp: int, pb: int) -> bool:   # :1169-1180
+        if lp < 0 or lp > 4 or lc < 0 or lc > 8 or pb < 0 or pb > 4:
+            return False
+        self._p.lc, self._p.lp, self._p.pb = lc, lp, pb
+        return True
+
+    def SetEndMarkerMode(self, endMarkerMode: bool):   # :1182-1184
+        self._p.eos = 1 if endMarkerMode else 0
+
+    def params(self) -> Params:
+        return Params(*[getattr(self._p, f) for f, _ in Params._fields_])
+
+    def WriteCoderProperties(self, outStream):   # :1079-1085
+        outStream.write(write_props(self._p))
+
+    def Code(self, inStream, outStream, inSize: int = -1, outSize: int = -1, progress=None):   # :1064-1077
+        data = _read_all(inStream)
+        ctx = self._ctx or default_context()
+        out = ctx.encode_batch([data], self._p)[0]
+        outStream.write(out)
+        if progress is not None:   # ICodeProgress.SetProgress, once at the end (no output bits depend on it)
+            progress.SetProgress(len(data), len(out))
+
+
+class Decoder:
+    """Mirror of SevenZip.Compression.LZMA.Decoder (Decoder.java:12-319)."""
+
+    def __init__(self, ctx: Optional[Context] = None):
+        self._ctx = ctx
+        self._props = None
+
+    def SetDecoderProperties(self, properties: bytes) -> bool:   # :303-318
+        if len(properties) < 5:
+            return False
+        if read_props(bytes(properties[:5])) is None:
+            return False
+        self._props = bytes(properties[:5])
+        return True
+
+    def Code(self, inStream, outStream, outSize: int) -> bool:   # :205-301
+        if self._props is None:
+            raise LzmaError(LZMA_E_PARAM, "SetDecoderProperties first")
+        data = _read_all(inStream)
+        ctx = self._ctx or default_context()
+        cap = outSize if outSize >= 0 else max(64 * len(data), 1 << 16)
+        while True:
+            st, out = ctx.decode_batch([data], self._props, [outSize], caps=[cap + 64])[0]
+            if st == LZMA_E_OVERFLOW and outSize < 0:
+                cap *= 4
+                continue
+            break
+        outStream.write(out)
+        return st == LZMA_OK
+
+
+# --------------------------------------------------------------------------
+# .lzma container (LzmaAlone.java:208-236) and multi-stream framing
+# --------------------------------------------------------------------------
+
+def lzma_header(p: Params, size: int) -> bytes:
+    """5 property bytes + 8-byte little-endian size (-1 with the end marker)."""
+    return write_props(p) + (size & 0xFFFFFFFFFFFFFFFF).to_bytes(8, "little")
+
+
+def compress_file_bytes(data: bytes, p: Params, ctx: Optional[Context] = None) -> bytes:
+    """LzmaAlone `e`: header + Encoder.Code output."""
+    ctx = ctx or default_context()
+    return lzma_header(p, -1 if p.eos else len(data)) + ctx.encode_batch([data], p)[0]
+
+
+def decompress_file_bytes(blob: bytes, ctx: Optional[Context] = None) -> bytes:
+    """LzmaAlone `d`: parse header, Decoder.Code; raises on corrupt data."""
+    if len(blob) < 13:
+        raise LzmaError(LZMA_E_DATA, "input .lzma file is too short")
+    d = Decoder(ctx)
+    if not d.SetDecoderProperties(blob[:5]):
+        raise LzmaError(LZMA_E_PARAM, "Incorrect stream properties")
+    size = int.from_bytes(blob[5:13], "little", signed=True)
+    import io
+    out = io.BytesIO()
+    if not d.Code(blob[13:], out, size):
+        raise LzmaError(LZMA_E_DATA, "Error in data stream")
+    return out.getvalue()
