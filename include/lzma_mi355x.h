@@ -14,6 +14,7 @@
  *   lzma_read_props       Decoder.SetDecoderProperties       Decoder.java:303-318
  *   lzma_encode           Encoder.Code (one stream)          Encoder.java:1064-1077
  *   lzma_enc_batch[_dev]  Encoder.Code on N independent streams
+ *   lzma_pack_dev         (framing) contiguous multi-stream container
  *   lzma_decode           Decoder.Code (one stream)          Decoder.java:205-301
  *   lzma_dec_batch[_dev]  Decoder.Code on N independent streams
  *   lzma_bench_generate   LzmaBench.CBenchRandomGenerator    LzmaBench.java:15-127
@@ -81,6 +82,11 @@ int lzma_enc_batch_dev(lzma_ctx *ctx, const lzma_params *p,
                        const uint8_t *d_in, const uint64_t *h_offs, int nstreams,
                        uint8_t *d_out, const uint64_t *h_out_offs, uint64_t *h_out_lens,
                        void *hip_stream);
+/* Gather stream i = d_src[h_src_offs[i] .. + h_lens[i]) to
+ * d_dst[h_dst_offs[i] ..), h_dst_offs = exclusive prefix sum of h_lens
+ * (nstreams+1 entries): packs capacity-layout encoder output. */
+int lzma_pack_dev(lzma_ctx *ctx, const uint8_t *d_src, const uint64_t *h_src_offs, const uint64_t *h_lens,
+                  int nstreams, uint8_t *d_dst, const uint64_t *h_dst_offs, void *hip_stream);
 /* Host buffers: out is packed, out_offs[nstreams+1] receives the layout. */
 int lzma_enc_batch(lzma_ctx *ctx, const lzma_params *p,
                    const uint8_t *in, const uint64_t *offs, int nstreams,

@@ -275,6 +275,7 @@ int run_match_finder(Ctx* ctx, const Derived& d, const uint8_t* in, const uint64
         if (bt4) hipLaunchKernelGGL((mf_keys_kernel<true>), dim3(grid_for(total, B)), dim3(B), 0, st, in, d_offs, nstreams, total, a);
         else hipLaunchKernelGGL((mf_keys_kernel<false>), dim3(grid_for(total, B)), dim3(B), 0, st, in, d_offs, nstreams, total, a);
     }
+    LZG_TRACE(ctx, st, "mf_keys done (%llu positions)", (unsigned long long)total);
     int rc;
     if (bt4) {
         {
@@ -302,6 +303,7 @@ int run_match_finder(Ctx* ctx, const Derived& d, const uint8_t* in, const uint64
         if (!t && tmp) return ctx->fail(LZMA_E_NOMEM, "select temp");
         hipcub::DeviceSelect::Flagged(t, tmp, it, w.flag, w.chain_start, w.counts + 1, (int)total, st);
     }
+    LZG_TRACE(ctx, st, "mf sorts + chain select done");
     uint64_t hc[2];
     hipMemcpyAsync(hc, w.counts, sizeof(hc), hipMemcpyDeviceToHost, st);
     if (hipStreamSynchronize(st) != hipSuccess) return ctx->fail(LZMA_E_DEVICE, "sync after chain select");
@@ -328,6 +330,7 @@ int run_match_finder(Ctx* ctx, const Derived& d, const uint8_t* in, const uint64
             else hipLaunchKernelGGL((mf_walk_kernel<uint32_t, false>), dim3(grid), dim3(WB), 0, st, in, d_offs, w.ks, w.vs, w.chain_order, w.chain_start, w.chain_len, w.counts + 1, a, w.son, (uint32_t*)w.pairs, w.ovf_off, (uint32_t*)w.ovf, w.ovf_used, w.ovf_cap, w.err);
         }
     }
+    LZG_TRACE(ctx, st, "mf_walk done (%llu chains)", (unsigned long long)nchains);
     int herr = 0;
     hipMemcpyAsync(&herr, w.err, sizeof(int), hipMemcpyDeviceToHost, st);
     if (hipStreamSynchronize(st) != hipSuccess) return ctx->fail(LZMA_E_DEVICE, "mf_walk: %s", hipGetErrorString(hipGetLastError()));

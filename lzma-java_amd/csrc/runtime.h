@@ -6,8 +6,14 @@
 #include <stdarg.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
 
+#include <chrono>
+
+#include <atomic>
 #include <map>
+#include <thread>
 #include <string>
 #include <vector>
 
@@ -51,6 +57,7 @@ struct TimedLaunch {
 struct Ctx {
     int device = 0;
     std::string err;
+    bool debug = getenv("LZMA_MI355X_DEBUG") != nullptr;   // phase trace on stderr (synchronises)
     uint64_t batch_bytes = 512ull << 20;
     // persistent workspace arena (grown, never shrunk)
     uint8_t* arena = nullptr;
@@ -116,6 +123,53 @@ struct Ctx {
     }
 };
 
+// debug trace: synchronise the stream and print a phase marker
+#define LZG_TRACE(ctx, st, ...)                                                     \
+    do {                                                                            \
+        if ((ctx)->debug) {                                                         \
+            hipError_t e_ = hipStreamSynchronize(st);                               \
+            fprintf(stderr, "[lzma-mi355x] ");                                      \
+            fprintf(stderr, __VA_ARGS__);                                           \
+            fprintf(stderr, " (%s)\n", hipGetErrorString(e_));                      \
+            fflush(stderr);                                                         \
+        }                                                                           \
+    } while (0)
+
+// Debug-only live view of a running kernel: the kernel stores checkpoints into
+// host-mapped memory; a host thread prints them until stop().
+struct DebugWatch {
+    uint32_t* host = nullptr;
+    uint32_t* dev = nullptr;
+    std::atomic<bool> run{false};
+    std::thread th;
+    void start(int words) {
+        if (hipHostMalloc((void**)&host, words * 4, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) { host = nullptr; return; }
+        memset(host, 0, words * 4);
+        hipHostGetDevicePointer((void**)&dev, host, 0);
+        run = true;
+        th = std::thread([this, words]() {
+            std::vector<uint32_t> last(words, 0);
+            while (run) {
+                std::this_thread::sleep_for(std::chrono::milliseconds(500));
+                bool ch = false;
+                for (int i = 0; i < words; i++) if (((volatile uint32_t*)host)[i] != last[i]) ch = true;
+                if (!ch) continue;
+                fprintf(stderr, "[lzma-mi355x dbg]");
+                for (int i = 0; i < words; i++) { last[i] = ((volatile uint32_t*)host)[i]; fprintf(stderr, " %u", last[i]); }
+                fprintf(stderr, "\n");
+                fflush(stderr);
+            }
+        });
+    }
+    void stop() {
+        if (!host) return;
+        run = false;
+        th.join();
+        hipHostFree(host);
+        host = dev = nullptr;
+    }
+};
+
 inline TimedLaunch::TimedLaunch(Ctx* c, const char* n, hipStream_t s) : ctx(c), name(n), st(s) {
     if (ctx->timing) { a = ctx->get_event(); b = ctx->get_event(); hipEventRecord(a, st); }
 }
@@ -159,7 +213,13 @@ struct EncArgs {
     uint64_t scratch_stride;
     uint32_t fb, lc, lp, pb, eos, dist_table_size, len_table_size;
     uint32_t lit_in_lds;
+    uint32_t* dbg;                // debug checkpoints (host-mapped, LZMA_MI355X_DEBUG only) or null
+    uint64_t* prof;               // phase cycles [nstreams][kProfSlots] (LZG_PROF builds) or null
 };
+
+// encoder phase profile slots (LZG_PROF builds)
+enum { PF_TOTAL, PF_GETOPT, PF_MATCHES, PF_REPLEN, PF_TWOLEN, PF_LIT, PF_RELAX, PF_TWOREL, PF_STATE, PF_BACK,
+       PF_ENCODE, PF_TABLES, PF_NOPT, PF_NPOS, kProfSlots };
 
 int launch_encoder(Ctx* ctx, const EncArgs& a, bool wide_pairs, int grid, hipStream_t st);
 uint32_t enc_lit_in_lds(const Derived& d);

@@ -44,6 +44,33 @@ static int check_device(Ctx* ctx) {
         if (e_ != hipSuccess) return ctx->fail(LZMA_E_DEVICE, "%s: %s", #x, hipGetErrorString(e_)); \
     } while (0)
 
+#ifdef LZG_PROF
+// Per-phase s_memtime cycles summed over the pass's streams (stderr).
+static void report_profile(const uint64_t* d_prof, int ns, uint64_t total, hipStream_t st) {
+    std::vector<uint64_t> h((size_t)ns * kProfSlots);
+    hipMemcpyAsync(h.data(), d_prof, h.size() * 8, hipMemcpyDeviceToHost, st);
+    hipStreamSynchronize(st);
+    static const char* names[kProfSlots] = {"total", "get_optimum", "match_lists", "rep_len", "two_step_len", "lit_price",
+                                            "relax", "two_step_relax", "state", "backward", "encode", "tables",
+                                            "n_getopt", "n_positions"};
+    double sum[kProfSlots] = {0};
+    uint64_t mx = 0;
+    for (int i = 0; i < ns; i++) {
+        for (int k = 0; k < kProfSlots; k++) sum[k] += (double)h[(size_t)i * kProfSlots + k];
+        mx = std::max(mx, h[(size_t)i * kProfSlots]);
+    }
+    fprintf(stderr, "[lzg prof] %d streams, %llu bytes, max stream cycles %llu\n", ns, (unsigned long long)total,
+            (unsigned long long)mx);
+    for (int k = 0; k < kProfSlots; k++)
+        fprintf(stderr, "[lzg prof] %-15s %16.0f  %8.1f per byte  %5.1f%%\n", names[k], sum[k], sum[k] / (double)total,
+                k < PF_NOPT ? 100.0 * sum[k] / std::max(sum[0], 1.0) : 0.0);
+}
+#endif
+
+// Parser scratch is ~160 KiB per stream (one workgroup each): cap a pass at
+// 16384 streams (~2.6 GB).
+constexpr int kMaxStreamsPerPass = 16384;
+
 // one encode pass over streams [s0, s1) of a batch
 static int encode_pass(Ctx* ctx, const Derived& d, const uint8_t* d_in, const uint64_t* h_offs, int s0, int s1,
                        uint8_t* d_out, const uint64_t* h_out_offs, uint64_t* h_out_lens, int32_t* h_status,
@@ -131,7 +158,22 @@ static int encode_pass(Ctx* ctx, const Derived& d, const uint8_t* d_in, const ui
         a.fb = d.fb; a.lc = d.lc; a.lp = d.lp; a.pb = d.pb; a.eos = d.eos;
         a.dist_table_size = d.dist_table_size; a.len_table_size = d.len_table_size;
         a.lit_in_lds = enc_lit_in_lds(d);
+        LZG_TRACE(ctx, st, "encode pass: %d streams, %llu bytes, grid %d", ns, (unsigned long long)total, grid);
+        DebugWatch watch;
+        if (ctx->debug) { watch.start(16); a.dbg = watch.dev; }
+#ifdef LZG_PROF
+        uint64_t* d_prof = nullptr;
+        HIPCHK(hipMalloc(&d_prof, (size_t)ns * kProfSlots * 8));
+        HIPCHK(hipMemsetAsync(d_prof, 0, (size_t)ns * kProfSlots * 8, st));
+        a.prof = d_prof;
+#endif
         if ((rc = launch_encoder(ctx, a, wide, grid, st))) return rc;
+        LZG_TRACE(ctx, st, "enc_parse done");
+        watch.stop();
+#ifdef LZG_PROF
+        report_profile(d_prof, ns, total, st);
+        hipFree(d_prof);
+#endif
         HIPCHK(hipMemcpyAsync(h_out_lens + s0, d_lens, ns * 8, hipMemcpyDeviceToHost, st));
         HIPCHK(hipMemcpyAsync(h_status + s0, d_status, ns * 4, hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
@@ -152,15 +194,21 @@ static int encode_batch_dev(Ctx* ctx, const lzma_params* p, const uint8_t* d_in,
     }
     std::vector<int32_t> status(nstreams, 0);
     int s0 = 0;
+    // h_out_lens doubles as a diagnostic for LZMA_E_INTERNAL: (reason << 32) | position
     while (s0 < nstreams) {
         int s1 = s0 + 1;
-        while (s1 < nstreams && h_offs[s1 + 1] - h_offs[s0] <= ctx->batch_bytes) s1++;
+        // bytes bound the match-finder workspace; the stream count bounds the
+        // per-workgroup parser scratch (one workgroup per stream)
+        while (s1 < nstreams && s1 - s0 < kMaxStreamsPerPass && h_offs[s1 + 1] - h_offs[s0] <= ctx->batch_bytes) s1++;
         int rc = encode_pass(ctx, d, d_in, h_offs, s0, s1, d_out, h_out_offs, h_out_lens, status.data(), st);
         if (rc) return rc;
         s0 = s1;
     }
     for (int i = 0; i < nstreams; i++)
-        if (status[i] != LZMA_OK) return ctx->fail(status[i], "stream %d: output capacity too small", i);
+        if (status[i] != LZMA_OK)
+            return ctx->fail(status[i], status[i] == LZMA_E_OVERFLOW ? "stream %d: output capacity too small%.0llu"
+                                                                     : "stream %d: encoder consistency check tripped (%llx)",
+                             i, (unsigned long long)h_out_lens[i]);
     return LZMA_OK;
 }
 
@@ -323,6 +371,33 @@ int lzma_enc_batch_dev(lzma_ctx* ctx, const lzma_params* p, const uint8_t* d_in,
     if (check_device(ctx)) return LZMA_E_NODEVICE;
     hipSetDevice(ctx->device);
     return encode_batch_dev(ctx, p, d_in, h_offs, nstreams, d_out, h_out_offs, h_out_lens, (hipStream_t)hip_stream);
+}
+
+int lzma_pack_dev(lzma_ctx* ctx, const uint8_t* d_src, const uint64_t* h_src_offs, const uint64_t* h_lens, int nstreams,
+                  uint8_t* d_dst, const uint64_t* h_dst_offs, void* hip_stream) {
+    if (!ctx || !h_src_offs || !h_lens || !h_dst_offs || nstreams < 0) return LZMA_E_PARAM;
+    if (check_device(ctx)) return LZMA_E_NODEVICE;
+    if (nstreams == 0) return LZMA_OK;
+    hipSetDevice(ctx->device);
+    hipStream_t st = (hipStream_t)hip_stream;
+    for (int i = 0; i < nstreams; i++)
+        if (h_dst_offs[i + 1] - h_dst_offs[i] != h_lens[i]) return ctx->fail(LZMA_E_PARAM, "dst offsets must be the prefix sum of lens");
+    Carver probe(nullptr);
+    probe.take<uint64_t>(nstreams + 1);
+    probe.take<uint64_t>(nstreams + 1);
+    if (!ctx->ensure_arena(probe.off + 4096)) return ctx->fail(LZMA_E_NOMEM, "pack workspace");
+    Carver c(ctx->arena);
+    uint64_t* d_so = c.take<uint64_t>(nstreams + 1);
+    uint64_t* d_do = c.take<uint64_t>(nstreams + 1);
+    HIPCHK(hipMemcpyAsync(d_so, h_src_offs, (nstreams + 1) * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(d_do, h_dst_offs, (nstreams + 1) * 8, hipMemcpyHostToDevice, st));
+    {
+        TimedLaunch tl(ctx, "pack", st);
+        hipLaunchKernelGGL(pack_kernel, dim3(std::min(nstreams, 65535)), dim3(256), 0, st, d_src, d_so, d_do, d_dst, nstreams);
+    }
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(st));
+    return LZMA_OK;
 }
 
 int lzma_enc_batch(lzma_ctx* ctx, const lzma_params* p, const uint8_t* in, const uint64_t* offs, int nstreams,

@@ -23,7 +23,8 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _PKG = os.path.dirname(_HERE)
-LIB_PATH = os.path.join(_PKG, "build", "liblzma_mi355x.so")
+# LZMA_AMD_LIB overrides the library path (e.g. the LZG_PROF profiling build)
+LIB_PATH = os.environ.get("LZMA_AMD_LIB") or os.path.join(_PKG, "build", "liblzma_mi355x.so")
 
 LZMA_OK = 0
 LZMA_E_PARAM = -1
@@ -38,6 +39,7 @@ EXPORTED_SYMBOLS = [
     "lzma_version", "lzma_params_default", "lzma_params_check", "lzma_write_props", "lzma_read_props",
     "lzma_enc_bound", "lzma_ctx_create", "lzma_ctx_destroy", "lzma_last_error", "lzma_ctx_set_batch_bytes",
     "lzma_ctx_set_timing", "lzma_ctx_timings", "lzma_ctx_reset_timings", "lzma_enc_batch_dev", "lzma_enc_batch",
+    "lzma_pack_dev",
     "lzma_encode", "lzma_dec_batch_dev", "lzma_dec_batch", "lzma_decode", "lzma_bench_generate",
 ]
 
@@ -67,6 +69,14 @@ def lib():
         if not os.path.exists(LIB_PATH):
             raise LzmaError(LZMA_E_INTERNAL, "%s not built (run `make -C lzma-java_amd` or "
                                              "__graft_entry__.build())" % LIB_PATH)
+        # PyTorch-ROCm wheels bundle their own libamdhip64 (SONAME
+        # libamdhip64.so.7). Load it first so our DT_NEEDED resolves to the same
+        # runtime: one HIP/HSA instance per process, and torch's hipStream_t
+        # handles are valid streams for the device-resident entry points.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = ctypes.CDLL(LIB_PATH)
         vp, u64, i32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int
         P = ctypes.POINTER(Params)
@@ -87,6 +97,7 @@ def lib():
         L.lzma_ctx_reset_timings.argtypes = [vp]
         L.lzma_enc_batch_dev.argtypes = [vp, P, vp, vp, i32, vp, vp, vp, vp]
         L.lzma_enc_batch.argtypes = [vp, P, vp, vp, i32, vp, u64, vp]
+        L.lzma_pack_dev.argtypes = [vp, vp, vp, vp, i32, vp, vp, vp]
         L.lzma_encode.argtypes = [vp, P, vp, u64, vp, u64, ctypes.POINTER(u64)]
         L.lzma_dec_batch_dev.argtypes = [vp, vp, vp, vp, i32, vp, vp, vp, vp, vp, vp]
         L.lzma_dec_batch.argtypes = [vp, vp, vp, vp, i32, vp, vp, vp, vp, vp]
@@ -232,6 +243,17 @@ class Context:
         self.check(lib().lzma_enc_batch_dev(self.h, ctypes.byref(p), _dptr(d_in), offs.ctypes.data, n, _dptr(d_out),
                                             out_offs.ctypes.data, lens.ctypes.data, ctypes.c_void_p(stream_ptr)))
         return lens[:n]
+
+    def pack_dev(self, d_src, src_offs: np.ndarray, lens: np.ndarray, d_dst, stream_ptr: int = 0) -> np.ndarray:
+        """Gather capacity-layout streams into a contiguous buffer; returns the packed offsets."""
+        n = len(lens)
+        src_offs = np.ascontiguousarray(src_offs, dtype=np.uint64)
+        lens = np.ascontiguousarray(lens, dtype=np.uint64)
+        dst = np.zeros(n + 1, dtype=np.uint64)
+        dst[1:] = np.cumsum(lens)
+        self.check(lib().lzma_pack_dev(self.h, _dptr(d_src), src_offs.ctypes.data, lens.ctypes.data, n, _dptr(d_dst),
+                                       dst.ctypes.data, ctypes.c_void_p(stream_ptr)))
+        return dst
 
     def decode_batch_dev(self, props: bytes, d_in, in_offs: np.ndarray, out_sizes: np.ndarray, d_out,
                          out_offs: np.ndarray, stream_ptr: int = 0):

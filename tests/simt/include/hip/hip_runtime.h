@@ -207,6 +207,31 @@ inline unsigned long long __ballot(int pred) {
     ::hipemu::barrier();
     return m;
 }
+#define __builtin_amdgcn_fence(order, scope) __atomic_signal_fence(__ATOMIC_SEQ_CST)
+#define __builtin_nontemporal_load(p) (*(p))
+#define __builtin_nontemporal_store(v, p) (*(p) = (v))
+struct __amdgpu_buffer_rsrc_t { uint8_t* base; uint32_t bytes; };
+inline __amdgpu_buffer_rsrc_t __builtin_amdgcn_make_buffer_rsrc(void* p, int, uint32_t bytes, uint32_t) {
+    return __amdgpu_buffer_rsrc_t{(uint8_t*)p, bytes};
+}
+inline uint32_t __builtin_amdgcn_raw_buffer_load_b32(__amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t soff, int) {
+    if ((uint64_t)off + soff + 4 > r.bytes) { fprintf(stderr, "hip-emu: buffer load out of range\n"); abort(); }
+    uint32_t v; memcpy(&v, r.base + off + soff, 4); return v;
+}
+inline void __builtin_amdgcn_raw_buffer_store_b32(uint32_t v, __amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t soff, int) {
+    if (off + soff + 4 > r.bytes) { fprintf(stderr, "hip-emu: buffer store out of range\n"); abort(); }
+    memcpy(r.base + off + soff, &v, 4);
+}
+inline uint8_t __builtin_amdgcn_raw_buffer_load_b8(__amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t soff, int) {
+    uint64_t o = (uint64_t)off + soff;
+    return o < r.bytes ? r.base[o] : 0;   // hardware range check: out of range reads 0
+}
+#define __HIP_MEMORY_SCOPE_SYSTEM 0
+#define __hip_atomic_store(p, v, order, scope) (*(p) = (v))
+enum { hipHostMallocMapped = 2, hipHostMallocCoherent = 0x40000000 };
+inline hipError_t hipHostMalloc(void** p, size_t n, unsigned) { *p = malloc(n); return *p ? hipSuccess : hipErrorMemoryAllocation; }
+inline hipError_t hipHostFree(void* p) { free(p); return hipSuccess; }
+inline hipError_t hipHostGetDevicePointer(void** d, void* h, unsigned) { *d = h; return hipSuccess; }
 inline int __ffsll(long long x) { return __builtin_ffsll(x); }
 inline int __clz(int x) { return __builtin_clz((unsigned)x); }
 inline unsigned atomicAdd(unsigned* p, unsigned v) { unsigned o = *p; *p = o + v; return o; }
