@@ -7,7 +7,9 @@ exactly as Encoder.Code would with the level-5 mapping:
 dict 2^26, fb 32, BT4, lc3 lp0 pb2. A step = encode every stream (GPU),
 pack the outputs into one contiguous container (GPU), decode every stream
 (GPU). Inputs are resident in HBM before the timed region. Scaling is weak:
-each rank processes its own 1 GiB with no data-path collective.
+each rank processes its own 1 GiB with no data-path collective; with N > 1
+ranks the step ends with the one exchange SURVEY.md 8(e) prescribes -- rank 0
+gathers every rank's packed streams over RCCL (lzma_amd.dist.gather_streams).
 
 Prints ONE JSON line (rank 0).
 """
@@ -23,6 +25,7 @@ import torch
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "lzma-java_amd"))
 import lzma_amd  # noqa: E402
+from lzma_amd import dist as lzdist  # noqa: E402
 
 HBM_PEAK = 8.0e12   # MI355X HBM3E, MI355X_MICROARCH.md chip-level parameters
 
@@ -35,7 +38,8 @@ def parse():
     ap.add_argument("--size", type=int, default=1 << 30, help="uncompressed bytes per GPU")
     ap.add_argument("--chunk", type=int, default=256 << 10, help="bytes per independent stream")
     ap.add_argument("--batch-bytes", type=int, default=512 << 20, help="input bytes per device pass")
-    ap.add_argument("--cpu-sample", type=int, default=8 << 20, help="bytes for the CPU baseline (0 = skip)")
+    ap.add_argument("--cpu-sample", type=int, default=32 << 20, help="bytes for the CPU baseline (0 = skip)")
+    ap.add_argument("--cpu-threads", type=int, default=16, help="threads for the multi-core CPU baseline")
     ap.add_argument("--no-verify", action="store_true")
     return ap.parse_args()
 
@@ -57,6 +61,8 @@ def main():
     # ---- synthetic data (host gen, then H2D; outside the timed region)
     size = args.size
     host = lzma_amd.bench_generate(size)
+    if rank:   # distinct streams per rank: the generator output rotated by a rank-dependent odd offset
+        host = np.roll(host, -(rank * 262147) % size)
     d_in = torch.from_numpy(host).to(dev)
     n = (size + args.chunk - 1) // args.chunk
     offs = np.minimum(np.arange(n + 1, dtype=np.uint64) * np.uint64(args.chunk), np.uint64(size))
@@ -80,6 +86,9 @@ def main():
         t0 = time.perf_counter()
         lens = ctx.encode_batch_dev(d_in, offs, p, d_comp, cap_offs, st)
         pk = ctx.pack_dev(d_comp, cap_offs, lens, d_pack, st)
+        if dist:   # the single data exchange: rank 0 collects every rank's packed streams
+            g, _, _ = lzdist.gather_streams(d_pack, lens, dst=0)
+            state["gathered"] = 0 if g is None else int(g.numel())
         t1 = time.perf_counter()
         dlens, dstat = ctx.decode_batch_dev(props, d_pack, pk, out_sizes, d_dec, offs, st)
         t2 = time.perf_counter()
@@ -140,8 +149,8 @@ def main():
                 "alg_bytes_per_launch": alg}
 
     cpu = None
-    if rank == 0 and args.cpu_sample > 0:
-        cpu = cpu_baseline(host, args.chunk, args.cpu_sample, p)
+    if rank == 0 and args.cpu_sample > 0 and world == 1:
+        cpu = cpu_baseline(host, args.chunk, args.cpu_sample, p, args.cpu_threads)
 
     if rank == 0:
         res = {
@@ -157,6 +166,7 @@ def main():
             "compress_MBps": size * world * args.steps / max(state["t_enc"], 1e-9) / 1e6,
             "decompress_MBps": size * world * args.steps / max(state["t_dec"], 1e-9) / 1e6,
             "ratio": comp_bytes / size, "verified": ok,
+            "gathered_bytes_rank0": state.get("gathered"),
             "kernels_ms": {k: {"total_ms": v[0], "launches": v[1]} for k, v in timings.items()},
             "roofline": roofline, "cpu_baseline": cpu,
         }
@@ -168,26 +178,46 @@ def main():
         sys.exit(1)
 
 
-def cpu_baseline(host, chunk, sample, p):
-    """C restatement of the reference (oracle/, 1 thread) on a bounded sample of
-    the same chunks: encode + decode, MB/s of uncompressed bytes."""
+def cpu_baseline(host, chunk, sample, p, threads):
+    """C restatement of the reference (oracle/) on a bounded sample of the same
+    chunks: encode + decode, MB/s of uncompressed bytes. Timed with 1 thread
+    (the reference is single-threaded) and with `threads` threads, one chunk
+    per task (ctypes releases the GIL inside the C calls); `value` is the
+    multi-thread figure."""
     sys.path.insert(0, os.path.join(REPO, "tests"))
     import oracle_ffi as orc
+    from concurrent.futures import ThreadPoolExecutor
     op = orc.params(p.dict_size, p.fb, p.mf, p.lc, p.lp, p.pb, p.eos)
     props = orc.props(op)
     sample = min(sample, host.size)
     chunks = [host[i:min(i + chunk, sample)].tobytes() for i in range(0, sample, chunk)]
-    t0 = time.perf_counter()
-    encs = [orc.encode(c, op) for c in chunks]
-    t1 = time.perf_counter()
-    for c, e in zip(chunks, encs):
+
+    def enc(c):
+        return orc.encode(c, op)
+
+    def dec(args):
+        c, e = args
         rc, d = orc.decode(e, props, len(c))
         assert rc == 1 and d == c
-    t2 = time.perf_counter()
-    return {"value": sample / (t2 - t0) / 1e6, "unit": "MB/s", "cores": 1, "kind": "port",
-            "compress_MBps": sample / (t1 - t0) / 1e6, "decompress_MBps": sample / (t2 - t1) / 1e6,
-            "sample": "first %d MiB of the same workload (%d streams of %d KiB), oracle/ C restatement, 1 thread"
-                      % (sample >> 20, len(chunks), chunk >> 10)}
+
+    def timed(nthreads):
+        with ThreadPoolExecutor(max_workers=nthreads) as ex:
+            t0 = time.perf_counter()
+            encs = list(ex.map(enc, chunks))
+            t1 = time.perf_counter()
+            list(ex.map(dec, zip(chunks, encs)))
+            t2 = time.perf_counter()
+        return sample / (t2 - t0) / 1e6, sample / (t1 - t0) / 1e6, sample / (t2 - t1) / 1e6
+
+    one = timed(1)
+    threads = max(1, min(threads, len(chunks)))
+    multi = timed(threads) if threads > 1 else one
+    return {"value": multi[0], "unit": "MB/s", "cores": threads, "kind": "port",
+            "compress_MBps": multi[1], "decompress_MBps": multi[2],
+            "single_thread": {"value": one[0], "compress_MBps": one[1], "decompress_MBps": one[2], "cores": 1},
+            "sample": "first %d MiB of the same workload (%d streams of %d KiB), oracle/ C restatement of the "
+                      "Java reference (no JDK on the box), %d threads; single_thread = 1 thread"
+                      % (sample >> 20, len(chunks), chunk >> 10, threads)}
 
 
 if __name__ == "__main__":
