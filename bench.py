@@ -37,7 +37,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--size", type=int, default=1 << 30, help="uncompressed bytes per GPU")
     ap.add_argument("--chunk", type=int, default=256 << 10, help="bytes per independent stream")
-    ap.add_argument("--batch-bytes", type=int, default=512 << 20, help="input bytes per device pass")
+    ap.add_argument("--batch-bytes", type=int, default=1 << 30,
+                    help="input bytes per device pass (1 GiB: all streams of a GPU in one encoder launch)")
     ap.add_argument("--cpu-sample", type=int, default=32 << 20, help="bytes for the CPU baseline (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=16, help="threads for the multi-core CPU baseline")
     ap.add_argument("--no-verify", action="store_true")

@@ -33,10 +33,15 @@ namespace lzg {
 
 static __constant__ Tables c_tab = make_tables();
 
-constexpr int kOptLds = 256;        // _optimum slots kept in LDS
-constexpr int kLitLdsMaxBits = 3;   // literal coders in LDS when lc + lp <= 3
+constexpr int kOptLds = 64;         // _optimum slots kept in LDS (deeper slots spill to HBM)
+constexpr int kLitLdsMaxBits = 1;   // literal coders in LDS when lc + lp <= 1 (<= 3 KiB); else HBM/L2
 constexpr int kMdCap = kMatchMaxLen + 1;
-constexpr int kRing = 64;           // match-info prefetch window (positions)
+constexpr int kRing = 32;           // match-info prefetch window (positions)
+constexpr int kGW = 64;             // gather window: offsets -1 .. kGW-2 around the current position
+constexpr int kGI = kGW / kWave;    // gather iterations per side (1 on hardware)
+constexpr int kSides = 7;           // cur, rep0..rep3, pair0, pair1
+constexpr int kObuf = 256;          // output staging ring (bytes, power of two)
+constexpr int kLitSlots = (8 + kWave - 1) / kWave;   // literal bits per lane (1 on hardware)
 
 #define FI __device__ __forceinline__
 // Lanes of one wavefront exchange data through LDS. The hardware runs one
@@ -61,13 +66,51 @@ constexpr int kRing = 64;           // match-info prefetch window (positions)
 #define PCOUNT(k) do {} while (0)
 #endif
 
+FI uint64_t uni64(uint64_t v) {
+    return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32)) << 32) |
+           (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+}
+
+// value of bit slot j (j < 8) held by lane j % kWave in register slot j / kWave
+template <int N>
+FI uint32_t lane_value(const uint32_t (&v)[N], int j) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)v[j / kWave], j % kWave);
+}
+
 FI uint32_t sel4(uint32_t i, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
     return i == 0 ? a : (i == 1 ? b : (i == 2 ? c : d));
 }
 
-template <typename PairT, bool LIT_LDS>
+// Encoder-side probability layout (the models of Encoder.java:113-128). The
+// posState-indexed models (isMatch, isRep0Long, the low/mid length coders) are
+// strided by 1 << PBS posStates: PBS = 2 serves pb <= 2 (the common case, and
+// 1.3 KiB less LDS per stream than the 16-posState layout), PBS = 4 serves pb 3-4.
+template <int PBS>
+struct ProbLayout {
+    static constexpr int IS_MATCH = 0;
+    static constexpr int IS_REP = IS_MATCH + (kNumStates << PBS);
+    static constexpr int G0 = IS_REP + kNumStates, G1 = G0 + kNumStates, G2 = G1 + kNumStates;
+    static constexpr int R0L = G2 + kNumStates;
+    static constexpr int PSLOT = R0L + (kNumStates << PBS);
+    static constexpr int PENC = PSLOT + (kNumLenToPosStates << kNumPosSlotBits);
+    static constexpr int ALIGN = PENC + (kNumFullDistances - kEndPosModelIndex);
+    static constexpr int LOW = 2, MID = LOW + (8 << PBS), HIGH = MID + (8 << PBS), LSIZE = HIGH + 256;
+    static constexpr int LEN = ALIGN + kAlignTableSize;
+    static constexpr int RLEN = LEN + LSIZE;
+    static constexpr int COUNT = RLEN + LSIZE;
+};
+__host__ __device__ inline uint32_t enc_prob_count(uint32_t pb) {
+    return pb <= 2 ? (uint32_t)ProbLayout<2>::COUNT : (uint32_t)ProbLayout<4>::COUNT;
+}
+
+template <typename PairT, bool LIT_LDS, int PBS>
 struct Enc {
     using PP = PairPack<PairT>;
+    using PL = ProbLayout<PBS>;
+    static constexpr int E_IS_MATCH = PL::IS_MATCH, E_IS_REP = PL::IS_REP, E_G0 = PL::G0, E_G1 = PL::G1,
+                         E_G2 = PL::G2, E_R0L = PL::R0L, E_PSLOT = PL::PSLOT, E_PENC = PL::PENC,
+                         E_ALIGN = PL::ALIGN, E_LEN = PL::LEN, E_RLEN = PL::RLEN, E_LOW = PL::LOW,
+                         E_MID = PL::MID, E_HIGH = PL::HIGH, E_COUNT = PL::COUNT;
     uint32_t lane;
     // ---- LDS
     uint16_t* pp;             // ProbPrices [512]
@@ -75,10 +118,10 @@ struct Enc {
     uint16_t* lit;            // literal coders (LDS or HBM by LIT_LDS)
     uint16_t* lenp;           // [2][npos * tsize]
     uint32_t* lenc;           // [2][16]
-    uint32_t* psp;            // _posSlotPrices [256]
-    uint32_t* dp;             // _distancesPrices [512]
+    uint16_t* psp;            // _posSlotPrices [256] (prices < 2^14: 16 bits suffice)
+    uint16_t* dp;             // _distancesPrices [512]
     uint32_t* ap;             // _alignPrices [16]
-    uint32_t* tp;             // tempPrices [128]
+    uint16_t* tp;             // tempPrices [128]
     uint16_t* md_len;
     uint32_t* md_dist;
     uint32_t* ring_info;      // [kRing]
@@ -89,6 +132,8 @@ struct Enc {
     int32_t* o_bp2;
     uint8_t* o_fs;
     uint32_t* o_backs;        // [4][kOptLds]
+    uint8_t* win;             // gather window [kSides][kGW]: cur side, reps 0-3, pairs 0-1
+    uint8_t* obuf;            // output staging ring [kObuf]
     __amdgpu_buffer_rsrc_t spill;   // _optimum slots >= kOptLds in HBM (9 fields x kNumOpts dwords)
     // ---- parameters
     uint32_t fb, lc, lp, pb, ps_mask, eos, dist_table_size, tsize;
@@ -119,6 +164,9 @@ struct Enc {
     uint32_t rd0, rd1, rd2, rd3;   // _repDistances
     uint32_t rp0, rp1, rp2, rp3;   // reps
     uint32_t match_price_count, align_price_count;
+    // ---- per-position gather (see gather()): p = current position, equality masks per side
+    uint32_t gp;
+    uint64_t gm0, gm1, gm2, gm3, gmp0, gmp1;
 #ifdef LZG_PROF
     uint64_t prof[kProfSlots];
 #endif
@@ -194,7 +242,9 @@ struct Enc {
             price += price_bit(p[idx], bit);
         }
         for (int o = 1; o < 8 && o < kWave; o <<= 1) price += __shfl_xor(price, o);
-        return __shfl(price, 0);
+        // readfirstlane (not a shuffle): the result is provably wave-uniform, so
+        // the compiler keeps every price comparison downstream a scalar branch
+        return (uint32_t)__builtin_amdgcn_readfirstlane((int)price);
     }
     FI uint32_t len_price(int which, uint32_t sym, uint32_t ps) const {
         return lenp[(which << pb) * tsize + ps * tsize + sym];
@@ -222,11 +272,91 @@ struct Enc {
         return (uint32_t)limit;
     }
 
+    // ------------------------------------------------------------ per-position gather
+    // Every byte compare of one parse position (InWindow.GetMatchLen calls at
+    // Encoder.java:393-399, 631-700, 759-772) reads the window at offsets
+    // o = -1 .. kGW-2 from p (the current byte) on the cur side and at
+    // p + o - dist - 1 on the rep / match sides. gather() issues all of those
+    // byte loads at once (one lane per offset, one memory round trip), keeps
+    // equality masks per side (bit o+1 = bytes equal at offset o) and stores
+    // the bytes in the LDS window for the literal-price lookups. Compares past
+    // the window fall back to match_len.
+    FI void gather(bool with_pairs) {
+        gp = mfpos - 1;
+        const uint32_t d0 = rp0 + 1, d1 = rp1 + 1, d2 = rp2 + 1, d3 = rp3 + 1;
+        const uint32_t e0 = num_pairs > 0 ? md_dist[0] + 1 : d0, e1 = num_pairs > 1 ? md_dist[1] + 1 : d0;
+        uint32_t va[kGI], v0[kGI], v1[kGI], v2[kGI], v3[kGI], w0[kGI], w1[kGI];
+#pragma unroll
+        for (int it = 0; it < kGI; it++) {
+            const uint32_t q = gp - 1 + (uint32_t)(it * kWave) + lane;
+            va[it] = in_byte(q);
+            v0[it] = in_byte(q - d0); v1[it] = in_byte(q - d1); v2[it] = in_byte(q - d2); v3[it] = in_byte(q - d3);
+            if (with_pairs) { w0[it] = in_byte(q - e0); w1[it] = in_byte(q - e1); }
+        }
+        gm0 = gm1 = gm2 = gm3 = gmp0 = gmp1 = 0;
+#pragma unroll
+        for (int it = 0; it < kGI; it++) {
+            const int sh = it * kWave;
+            const uint32_t k = (uint32_t)sh + lane;
+            gm0 |= (uint64_t)__ballot(va[it] == v0[it]) << sh;
+            gm1 |= (uint64_t)__ballot(va[it] == v1[it]) << sh;
+            gm2 |= (uint64_t)__ballot(va[it] == v2[it]) << sh;
+            gm3 |= (uint64_t)__ballot(va[it] == v3[it]) << sh;
+            win[k] = (uint8_t)va[it];
+            win[1 * kGW + k] = (uint8_t)v0[it]; win[2 * kGW + k] = (uint8_t)v1[it];
+            win[3 * kGW + k] = (uint8_t)v2[it]; win[4 * kGW + k] = (uint8_t)v3[it];
+            if (with_pairs) {
+                gmp0 |= (uint64_t)__ballot(va[it] == w0[it]) << sh;
+                gmp1 |= (uint64_t)__ballot(va[it] == w1[it]) << sh;
+                win[5 * kGW + k] = (uint8_t)w0[it]; win[6 * kGW + k] = (uint8_t)w1[it];
+            }
+        }
+        LANE_FENCE();
+    }
+    // byte at p + o on the cur side
+    FI uint32_t a_byte(int32_t o) const {
+        return (o >= -1 && o <= kGW - 2) ? (uint32_t)win[o + 1] : in_byte(gp + (uint32_t)o);
+    }
+    // byte at p + o - dist - 1 (side 1..6 = rep0..3, pair0..1; side < 0: not gathered)
+    FI uint32_t b_byte(int side, uint32_t dist, int32_t o) const {
+        return (side > 0 && o >= -1 && o <= kGW - 2) ? (uint32_t)win[side * kGW + o + 1]
+                                                       : in_byte(gp + (uint32_t)o - dist - 1);
+    }
+    // InWindow.GetMatchLen(index = o - 1, dist, limit) from the side's mask; the
+    // part of the compare beyond the window continues with match_len.
+    FI uint32_t glen(uint64_t m, uint32_t dist, int32_t o, int32_t limit) {
+        const int64_t rem = (int64_t)n - ((int64_t)gp + o);
+        if (limit > rem) limit = (int32_t)rem;
+        if (limit <= 0) return 0;
+        const int b = o + 1;                       // 0 <= b <= kGW
+        uint32_t r;
+        if (b >= kGW) r = 0;
+        else {
+            const uint64_t x = ~m >> b;            // bits past the window shift in as 0 (= "equal")
+            const uint32_t lim_w = (uint32_t)(kGW - b);
+            r = x ? (uint32_t)__builtin_ctzll(x) : 64u;
+            if (r > lim_w) r = lim_w;
+        }
+        if (r >= (uint32_t)limit) return (uint32_t)limit;
+        if ((uint32_t)b + r < (uint32_t)kGW) return r;   // mismatch inside the window
+        return r + match_len(o + (int32_t)r - 1, dist, limit - (int32_t)r);
+    }
+
     // ------------------------------------------------------------ range encoder (RangeEncoder.java:38-87)
+    // Output bytes are staged in LDS and written kObuf at a time by all lanes:
+    // a global store per byte would make the next dependent load wait for it
+    // (vmcnt counts stores and loads alike on CDNA).
+    FI void flush_out(uint64_t start, uint32_t count) {
+        LANE_FENCE();
+        for (uint32_t i = lane; i < count; i += kWave)
+            if (start + i < cap) out[start + i] = obuf[i];
+        LANE_FENCE();
+    }
     FI void put_byte(uint32_t b) {
-        if (outpos < cap) { if (lane == 0) out[outpos] = (uint8_t)b; }
-        else overflow = 1;
+        if (outpos >= cap) overflow = 1;
+        if (lane == 0) obuf[outpos & (kObuf - 1)] = (uint8_t)b;
         outpos++;
+        if ((outpos & (kObuf - 1)) == 0) flush_out(outpos - kObuf, kObuf);
     }
     FI void shift_low() {
         uint32_t hi = (uint32_t)(low >> 32);
@@ -260,45 +390,74 @@ struct Enc {
         uint32_t m = 1;
         for (int i = 0; i < nbits; i++) { uint32_t bit = sym & 1; rc_bit(p, m, bit); m = (m << 1) | bit; sym >>= 1; }
     }
-    FI void lit_encode(uint16_t* p, uint32_t sym) {   // LiteralEncoder.java:17-24
-        uint32_t ctx = 1;
-        for (int i = 7; i >= 0; i--) { uint32_t bit = (sym >> i) & 1; rc_bit(p, ctx, bit); ctx = (ctx << 1) | bit; }
-    }
-    FI void lit_encode_matched(uint16_t* p, uint32_t mb, uint32_t sym) {   // LiteralEncoder.java:26-40
-        uint32_t ctx = 1;
-        bool same = true;
-        for (int i = 7; i >= 0; i--) {
-            uint32_t bit = (sym >> i) & 1, st = ctx;
-            if (same) { uint32_t mbit = (mb >> i) & 1; st += (1 + mbit) << 8; same = (mbit == bit); }
-            rc_bit(p, st, bit);
-            ctx = (ctx << 1) | bit;
+    // LiteralEncoder.Encoder2.encode / encodeMatched (LiteralEncoder.java:17-40).
+    // The 8 model indices depend only on (sym, mb), and they are distinct, so
+    // the probabilities are read in one step (lane j <-> bit 7-j), the range
+    // coder runs on the register copies, and lanes write the updated models
+    // back in one step: one memory round trip per literal even when the
+    // coders live in HBM.
+    FI void lit_encode(uint16_t* p, bool matched, uint32_t mb, uint32_t sym) {
+        int first = -1;
+        if (matched) {
+            const uint32_t diff = (mb ^ sym) & 0xFFu;
+            first = diff ? 31 - __clz(diff) : -1;
         }
+        uint32_t pr[kLitSlots], ix[kLitSlots];
+#pragma unroll
+        for (int t = 0; t < kLitSlots; t++) {
+            const int j = t * kWave + (int)lane;
+            ix[t] = 0; pr[t] = 0;
+            if (j < 8) {
+                const int i = 7 - j;
+                const uint32_t ctx = (0x100u | sym) >> (i + 1);
+                ix[t] = (matched && i >= first) ? ((1 + ((mb >> i) & 1)) << 8) + ctx : ctx;
+                pr[t] = p[ix[t]];
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const uint32_t prob = lane_value(pr, j);
+            const uint32_t bound = (range >> 11) * prob;
+            if ((sym >> (7 - j)) & 1) { low += bound; range -= bound; }
+            else range = bound;
+            if ((range & kTopMask) == 0) { range <<= 8; shift_low(); }
+        }
+#pragma unroll
+        for (int t = 0; t < kLitSlots; t++) {
+            const int j = t * kWave + (int)lane;
+            if (j < 8) {
+                const uint32_t q = pr[t];
+                p[ix[t]] = (uint16_t)(((sym >> (7 - j)) & 1) ? q - (q >> kNumMoveBits)
+                                                            : q + ((kBitModelTotal - q) >> kNumMoveBits));
+            }
+        }
+        LANE_FENCE();
     }
 
     // ------------------------------------------------------------ price tables
     FI void update_len_table(int which, uint32_t ps) {   // LenEncoder.SetPrices + LenPriceTableEncoder.UpdateTable
-        const uint16_t* L = probs + (which ? P_REP_LEN : P_LEN);
+        const uint16_t* L = probs + (which ? E_RLEN : E_LEN);
         uint32_t a0 = price0(L[LEN_CHOICE]), a1 = price1(L[LEN_CHOICE]);
         uint32_t b0 = a1 + price0(L[LEN_CHOICE + 1]), b1 = a1 + price1(L[LEN_CHOICE + 1]);
         uint16_t* dst = lenp + (which << pb) * tsize + ps * tsize;
         for (uint32_t i = lane; i < tsize; i += kWave) {
             uint32_t pr;
-            if (i < (uint32_t)kNumLowLenSymbols) pr = a0 + bt_price(L + LEN_LOW + ps * 8, 3, i);
-            else if (i < (uint32_t)(kNumLowLenSymbols + kNumMidLenSymbols)) pr = b0 + bt_price(L + LEN_MID + ps * 8, 3, i - kNumLowLenSymbols);
-            else pr = b1 + bt_price(L + LEN_HIGH, 8, i - kNumLowLenSymbols - kNumMidLenSymbols);
+            if (i < (uint32_t)kNumLowLenSymbols) pr = a0 + bt_price(L + E_LOW + ps * 8, 3, i);
+            else if (i < (uint32_t)(kNumLowLenSymbols + kNumMidLenSymbols)) pr = b0 + bt_price(L + E_MID + ps * 8, 3, i - kNumLowLenSymbols);
+            else pr = b1 + bt_price(L + E_HIGH, 8, i - kNumLowLenSymbols - kNumMidLenSymbols);
             dst[i] = (uint16_t)pr;
         }
         lenc[which * 16 + ps] = tsize;
         LANE_FENCE();
     }
     FI void len_encode(int which, uint32_t sym, uint32_t ps) {   // LenEncoder.java:24-39 + LenPriceTableEncoder.java:31-37
-        uint16_t* L = probs + (which ? P_REP_LEN : P_LEN);
-        if (sym < (uint32_t)kNumLowLenSymbols) { rc_bit(L, LEN_CHOICE, 0); bt_enc(L + LEN_LOW + ps * 8, 3, sym); }
+        uint16_t* L = probs + (which ? E_RLEN : E_LEN);
+        if (sym < (uint32_t)kNumLowLenSymbols) { rc_bit(L, LEN_CHOICE, 0); bt_enc(L + E_LOW + ps * 8, 3, sym); }
         else {
             sym -= kNumLowLenSymbols;
             rc_bit(L, LEN_CHOICE, 1);
-            if (sym < (uint32_t)kNumMidLenSymbols) { rc_bit(L, LEN_CHOICE + 1, 0); bt_enc(L + LEN_MID + ps * 8, 3, sym); }
-            else { rc_bit(L, LEN_CHOICE + 1, 1); bt_enc(L + LEN_HIGH, 8, sym - kNumMidLenSymbols); }
+            if (sym < (uint32_t)kNumMidLenSymbols) { rc_bit(L, LEN_CHOICE + 1, 0); bt_enc(L + E_MID + ps * 8, 3, sym); }
+            else { rc_bit(L, LEN_CHOICE + 1, 1); bt_enc(L + E_HIGH, 8, sym - kNumMidLenSymbols); }
         }
         uint32_t c = lenc[which * 16 + ps] - 1;
         lenc[which * 16 + ps] = c;
@@ -307,27 +466,27 @@ struct Enc {
     FI void fill_distances_prices() {   // Encoder.java:1087-1118
         for (uint32_t i = kStartPosModelIndex + lane; i < (uint32_t)kNumFullDistances; i += kWave) {
             uint32_t ps = c_tab.fastpos[i], footer = (ps >> 1) - 1, base = (2 | (ps & 1)) << footer;
-            tp[i] = rev_price(probs + P_POS_ENC + (int32_t)(base - ps - 1), (int)footer, i - base);
+            tp[i] = (uint16_t)rev_price(probs + E_PENC + (int32_t)(base - ps - 1), (int)footer, i - base);
         }
         for (uint32_t l = 0; l < (uint32_t)kNumLenToPosStates; l++) {
             uint32_t st = l << kNumPosSlotBits;
             for (uint32_t ps = lane; ps < dist_table_size; ps += kWave) {
-                uint32_t pr = bt_price(probs + P_POS_SLOT + st, kNumPosSlotBits, ps);
+                uint32_t pr = bt_price(probs + E_PSLOT + st, kNumPosSlotBits, ps);
                 if (ps >= (uint32_t)kEndPosModelIndex) pr += (((ps >> 1) - 1) - kNumAlignBits) << 6;
-                psp[st + ps] = pr;
+                psp[st + ps] = (uint16_t)pr;
             }
         }
         LANE_FENCE();
         for (uint32_t l = 0; l < (uint32_t)kNumLenToPosStates; l++) {
             uint32_t st = l << kNumPosSlotBits, st2 = l * kNumFullDistances;
             for (uint32_t i = lane; i < (uint32_t)kNumFullDistances; i += kWave)
-                dp[st2 + i] = i < (uint32_t)kStartPosModelIndex ? psp[st + i] : psp[st + c_tab.fastpos[i]] + tp[i];
+                dp[st2 + i] = (uint16_t)(i < (uint32_t)kStartPosModelIndex ? psp[st + i] : psp[st + c_tab.fastpos[i]] + tp[i]);
         }
         match_price_count = 0;
         LANE_FENCE();
     }
     FI void fill_align_prices() {   // Encoder.java:1120-1125
-        for (uint32_t i = lane; i < (uint32_t)kAlignTableSize; i += kWave) ap[i] = rev_price(probs + P_ALIGN, kNumAlignBits, i);
+        for (uint32_t i = lane; i < (uint32_t)kAlignTableSize; i += kWave) ap[i] = rev_price(probs + E_ALIGN, kNumAlignBits, i);
         align_price_count = 0;
         LANE_FENCE();
     }
@@ -375,17 +534,17 @@ struct Enc {
         if (num > 0) { mfpos += num; additional_offset += (int32_t)num; }
     }
     FI uint32_t rep_len1_price(uint32_t st, uint32_t ps) const {
-        return price0(probs[P_IS_REP_G0 + st]) + price0(probs[P_IS_REP0_LONG + (st << 4) + ps]);
+        return price0(probs[E_G0 + st]) + price0(probs[E_R0L + (st << PBS) + ps]);
     }
     FI uint32_t pure_rep_price(uint32_t ri, uint32_t st, uint32_t ps) const {
         uint32_t price;
         if (ri == 0) {
-            price = price0(probs[P_IS_REP_G0 + st]);
-            price += price1(probs[P_IS_REP0_LONG + (st << 4) + ps]);
+            price = price0(probs[E_G0 + st]);
+            price += price1(probs[E_R0L + (st << PBS) + ps]);
         } else {
-            price = price1(probs[P_IS_REP_G0 + st]);
-            if (ri == 1) price += price0(probs[P_IS_REP_G1 + st]);
-            else { price += price1(probs[P_IS_REP_G1 + st]); price += price_bit(probs[P_IS_REP_G2 + st], ri - 2); }
+            price = price1(probs[E_G0 + st]);
+            if (ri == 1) price += price0(probs[E_G1 + st]);
+            else { price += price1(probs[E_G1 + st]); price += price_bit(probs[E_G2 + st], ri - 2); }
         }
         return price;
     }
@@ -394,12 +553,12 @@ struct Enc {
     }
     FI uint32_t dist_price(uint32_t pos, uint32_t len) const {   // GetPosLenPrice without the length part
         uint32_t lps = len_to_pos_state(len);
-        if (pos < (uint32_t)kNumFullDistances) return dp[lps * kNumFullDistances + pos];
+        if (pos < (uint32_t)kNumFullDistances) return (uint32_t)dp[lps * kNumFullDistances + pos];
         uint32_t slot2;
         if (pos < (1u << 17)) slot2 = c_tab.fastpos[pos >> 6] + 12;
         else if (pos < (1u << 27)) slot2 = c_tab.fastpos[pos >> 16] + 32;
         else slot2 = c_tab.fastpos[pos >> 26] + 52;
-        return psp[(lps << kNumPosSlotBits) + slot2] + ap[pos & kAlignMask];
+        return (uint32_t)psp[(lps << kNumPosSlotBits) + slot2] + ap[pos & kAlignMask];
     }
     FI uint32_t pos_len_price(uint32_t pos, uint32_t len, uint32_t ps) const {   // Encoder.java:323-333
         return dist_price(pos, len) + len_price(0, len - kMatchMinLen, ps);
@@ -514,10 +673,11 @@ struct Enc {
         rp0 = rd0; rp1 = rd1; rp2 = rd2; rp3 = rd3;
         PCOUNT(PF_NOPT);
         PBEGIN(t0);
-        uint32_t rl0 = match_len(-1, rp0, kMatchMaxLen);
-        uint32_t rl1 = match_len(-1, rp1, kMatchMaxLen);
-        uint32_t rl2 = match_len(-1, rp2, kMatchMaxLen);
-        uint32_t rl3 = match_len(-1, rp3, kMatchMaxLen);
+        gather(false);
+        uint32_t rl0 = glen(gm0, rp0, 0, kMatchMaxLen);
+        uint32_t rl1 = glen(gm1, rp1, 0, kMatchMaxLen);
+        uint32_t rl2 = glen(gm2, rp2, 0, kMatchMaxLen);
+        uint32_t rl3 = glen(gm3, rp3, 0, kMatchMaxLen);
         PEND(PF_REPLEN, t0);
         uint32_t rep_max = 0, rl_max = rl0;
         if (rl1 > rl_max) { rep_max = 1; rl_max = rl1; }
@@ -533,18 +693,18 @@ struct Enc {
             move_pos(len_main - 1);
             return len_main;
         }
-        uint32_t cur_byte = byte_at(-1);
-        uint32_t match_byte = byte_at((int32_t)(0 - rd0 - 1 - 1));
+        uint32_t cur_byte = a_byte(0);
+        uint32_t match_byte = b_byte(1, rp0, 0);   // rp0 == rd0 here
         if (len_main < 2 && cur_byte != match_byte && rl_max < 2) { *back_res = -1; return 1; }
 
         set_fs(0, (fs_at(0) & 0xFu) | (state << 4));
         uint32_t pos_state = position & ps_mask;
         PBEGIN(t1);
-        uint32_t p1 = price0(probs[P_IS_MATCH + (state << 4) + pos_state]) +
+        uint32_t p1 = price0(probs[E_IS_MATCH + (state << PBS) + pos_state]) +
                       lit_price(lit_coder(position, prev_byte), !st_is_char(state), match_byte, cur_byte);
         PEND(PF_LIT, t1);
-        uint32_t match_price = price1(probs[P_IS_MATCH + (state << 4) + pos_state]);
-        uint32_t rep_match_price = match_price + price1(probs[P_IS_REP + state]);
+        uint32_t match_price = price1(probs[E_IS_MATCH + (state << PBS) + pos_state]);
+        uint32_t rep_match_price = match_price + price1(probs[E_IS_REP + state]);
         int32_t bp1 = -1;
         if (match_byte == cur_byte) {
             uint32_t srp = rep_match_price + rep_len1_price(state, pos_state);
@@ -567,7 +727,7 @@ struct Enc {
             if (rl < 2) continue;
             relax_rep(0, 2, rl, rep_match_price + pure_rep_price(i, state, pos_state), pos_state, 0, i);
         }
-        uint32_t normal_match_price = match_price + price0(probs[P_IS_REP + state]);
+        uint32_t normal_match_price = match_price + price0(probs[E_IS_REP + state]);
         uint32_t lstart = rl0 >= 2 ? rl0 + 1 : 2;
         if (lstart <= len_main) {
             // no look-ahead in this loop: every length is independent
@@ -651,13 +811,16 @@ struct Enc {
             set_fs(cur, (fsc & 0xFu) | (st << 4));
             set_back(cur, 0, rp0); set_back(cur, 1, rp1); set_back(cur, 2, rp2); set_back(cur, 3, rp3);
             uint32_t cur_price = price_at(cur);
-            uint32_t cur_byte = byte_at(-1);
-            uint32_t match_byte = byte_at((int32_t)(0 - rp0 - 1 - 1));
             uint32_t pos_state = position & ps_mask;
             PEND(PF_STATE, ts);
+            PBEGIN(tg);
+            gather(true);
+            PEND(PF_REPLEN, tg);
+            uint32_t cur_byte = a_byte(0);
+            uint32_t match_byte = b_byte(1, rp0, 0);
             PBEGIN(tl);
-            uint32_t cur_and1 = cur_price + price0(probs[P_IS_MATCH + (st << 4) + pos_state]) +
-                                lit_price(lit_coder(position, byte_at(-2)), !st_is_char(st), match_byte, cur_byte);
+            uint32_t cur_and1 = cur_price + price0(probs[E_IS_MATCH + (st << PBS) + pos_state]) +
+                                lit_price(lit_coder(position, a_byte(-1)), !st_is_char(st), match_byte, cur_byte);
             PEND(PF_LIT, tl);
             PBEGIN(tn);
             uint32_t nx = cur + 1;
@@ -670,8 +833,8 @@ struct Enc {
                 set_price(nx, nx_price); set_pp(nx, nx_pp); set_bp(nx, -1); set_fs(nx, fs_at(nx) & ~1u);
                 next_is_char = true;
             }
-            uint32_t match_price = cur_price + price1(probs[P_IS_MATCH + (st << 4) + pos_state]);
-            uint32_t rep_match_price = match_price + price1(probs[P_IS_REP + st]);
+            uint32_t match_price = cur_price + price1(probs[E_IS_MATCH + (st << PBS) + pos_state]);
+            uint32_t rep_match_price = match_price + price1(probs[E_IS_REP + st]);
             if (match_byte == cur_byte && !((nx_pp & 0xFFFFu) < cur && nx_bp == 0)) {
                 uint32_t srp = rep_match_price + rep_len1_price(st, pos_state);
                 if (srp <= nx_price) {
@@ -689,13 +852,13 @@ struct Enc {
             if (!next_is_char && match_byte != cur_byte) {   // literal + rep0
                 uint32_t t = num_avail_full - 1 < fb ? num_avail_full - 1 : fb;
                 PBEGIN(t2a);
-                uint32_t lt2 = match_len(0, rp0, (int32_t)t);
+                uint32_t lt2 = glen(gm0, rp0, 1, (int32_t)t);
                 PEND(PF_TWOLEN, t2a);
                 if (lt2 >= 2) {
                     PBEGIN(t2b);
                     uint32_t st2 = st_lit(st);
                     uint32_t psn = (position + 1) & ps_mask;
-                    uint32_t nrmp = cur_and1 + price1(probs[P_IS_MATCH + (st2 << 4) + psn]) + price1(probs[P_IS_REP + st2]);
+                    uint32_t nrmp = cur_and1 + price1(probs[E_IS_MATCH + (st2 << PBS) + psn]) + price1(probs[E_IS_REP + st2]);
                     uint32_t offset = cur + 1 + lt2;
                     extend_to(len_end, offset);
                     relax_two_step(offset, nrmp + rep_price(0, lt2, st2, psn), cur + 1, false, 0, 0);
@@ -706,8 +869,9 @@ struct Enc {
 #pragma unroll
             for (uint32_t ri = 0; ri < (uint32_t)kNumRepDistances; ri++) {
                 uint32_t rdist = sel4(ri, rp0, rp1, rp2, rp3);
+                const uint64_t gmr = ri == 0 ? gm0 : (ri == 1 ? gm1 : (ri == 2 ? gm2 : gm3));
                 PBEGIN(tr);
-                uint32_t lt = match_len(-1, rdist, (int32_t)num_avail);
+                uint32_t lt = glen(gmr, rdist, 0, (int32_t)num_avail);
                 PEND(PF_REPLEN, tr);
                 if (lt < 2) continue;
                 PBEGIN(trr);
@@ -719,19 +883,19 @@ struct Enc {
                     uint32_t t = num_avail_full - 1 - lt;
                     if (t > fb) t = fb;
                     PBEGIN(tq);
-                    uint32_t lt2 = match_len((int32_t)lt, rdist, (int32_t)t);
+                    uint32_t lt2 = glen(gmr, rdist, (int32_t)lt + 1, (int32_t)t);
                     PEND(PF_TWOLEN, tq);
                     if (lt2 >= 2) {
                         PBEGIN(tq2);
                         uint32_t st2 = st_long(st);
                         uint32_t psn = (position + lt) & ps_mask;
                         uint32_t clcp = rep_match_price + rep_price(ri, lt, st, pos_state) +
-                                        price0(probs[P_IS_MATCH + (st2 << 4) + psn]) +
-                                        lit_price(lit_coder(position + lt, byte_at((int32_t)lt - 2)), true,
-                                                  byte_at((int32_t)lt - 1 - (int32_t)(rdist + 1)), byte_at((int32_t)lt - 1));
+                                        price0(probs[E_IS_MATCH + (st2 << PBS) + psn]) +
+                                        lit_price(lit_coder(position + lt, a_byte((int32_t)lt - 1)), true,
+                                                  b_byte(1 + (int)ri, rdist, (int32_t)lt), a_byte((int32_t)lt));
                         st2 = st_lit(st2);
                         psn = (position + lt + 1) & ps_mask;
-                        uint32_t nrmp = clcp + price1(probs[P_IS_MATCH + (st2 << 4) + psn]) + price1(probs[P_IS_REP + st2]);
+                        uint32_t nrmp = clcp + price1(probs[E_IS_MATCH + (st2 << PBS) + psn]) + price1(probs[E_IS_REP + st2]);
                         uint32_t offset = lt + 1 + lt2;
                         extend_to(len_end, cur + offset);
                         relax_two_step(cur + offset, nrmp + rep_price(0, lt2, st2, psn), cur + lt + 1, true, cur, (int32_t)ri);
@@ -751,7 +915,7 @@ struct Enc {
 #ifdef LZG_PROF
                 uint64_t tm = PCLK();
 #endif
-                uint32_t normal_match_price = match_price + price0(probs[P_IS_REP + st]);
+                uint32_t normal_match_price = match_price + price0(probs[E_IS_REP + st]);
                 extend_to(len_end, cur + new_len);
                 uint32_t offs = 0;
                 while (offs + 1 < npairs && start_len > md_len[offs]) offs++;
@@ -770,19 +934,21 @@ struct Enc {
                         uint32_t t = num_avail_full - 1 - lt;
                         if (t > fb) t = fb;
                         PBEGIN(tm2);
-                        uint32_t lt2 = match_len((int32_t)lt, cur_back, (int32_t)t);
+                        const int side = offs < 2 ? 5 + (int)offs : -1;
+                        uint32_t lt2 = side > 0 ? glen(offs == 0 ? gmp0 : gmp1, cur_back, (int32_t)lt + 1, (int32_t)t)
+                                                : match_len((int32_t)lt, cur_back, (int32_t)t);
                         PEND(PF_TWOLEN, tm2);
                         if (lt2 >= 2) {
                             PBEGIN(tm3);
                             uint32_t cl = normal_match_price + pos_len_price(cur_back, lt, pos_state);
                             uint32_t st2 = st_match(st);
                             uint32_t psn = (position + lt) & ps_mask;
-                            uint32_t clcp = cl + price0(probs[P_IS_MATCH + (st2 << 4) + psn]) +
-                                            lit_price(lit_coder(position + lt, byte_at((int32_t)lt - 2)), true,
-                                                      byte_at((int32_t)lt - (int32_t)(cur_back + 1) - 1), byte_at((int32_t)lt - 1));
+                            uint32_t clcp = cl + price0(probs[E_IS_MATCH + (st2 << PBS) + psn]) +
+                                            lit_price(lit_coder(position + lt, a_byte((int32_t)lt - 1)), true,
+                                                      b_byte(side, cur_back, (int32_t)lt), a_byte((int32_t)lt));
                             st2 = st_lit(st2);
                             psn = (position + lt + 1) & ps_mask;
-                            uint32_t nrmp = clcp + price1(probs[P_IS_MATCH + (st2 << 4) + psn]) + price1(probs[P_IS_REP + st2]);
+                            uint32_t nrmp = clcp + price1(probs[E_IS_MATCH + (st2 << PBS) + psn]) + price1(probs[E_IS_REP + st2]);
                             uint32_t offset = lt + 1 + lt2;
                             extend_to(len_end, cur + offset);
                             relax_two_step(cur + offset, nrmp + rep_price(0, lt2, st2, psn), cur + lt + 1, true, cur,
@@ -800,14 +966,14 @@ struct Enc {
 
     // ------------------------------------------------------------ emitters (Encoder.java:938-1024, 818-841)
     FI void encode_rep(int32_t pos, uint32_t len, uint32_t ps, uint32_t cs) {
-        rc_bit(probs + P_IS_REP, state, 1);
+        rc_bit(probs + E_IS_REP, state, 1);
         if (pos == 0) {
-            rc_bit(probs + P_IS_REP_G0, state, 0);
-            rc_bit(probs + P_IS_REP0_LONG, cs, len == 1 ? 0 : 1);
+            rc_bit(probs + E_G0, state, 0);
+            rc_bit(probs + E_R0L, cs, len == 1 ? 0 : 1);
         } else {
-            rc_bit(probs + P_IS_REP_G0, state, 1);
-            if (pos == 1) rc_bit(probs + P_IS_REP_G1, state, 0);
-            else { rc_bit(probs + P_IS_REP_G1, state, 1); rc_bit(probs + P_IS_REP_G2, state, (uint32_t)pos - 2); }
+            rc_bit(probs + E_G0, state, 1);
+            if (pos == 1) rc_bit(probs + E_G1, state, 0);
+            else { rc_bit(probs + E_G1, state, 1); rc_bit(probs + E_G2, state, (uint32_t)pos - 2); }
         }
         if (len == 1) state = st_short(state);
         else { len_encode(1, len - kMatchMinLen, ps); state = st_long(state); }
@@ -816,7 +982,7 @@ struct Enc {
         else if (pos == 3) { uint32_t t = rd3; rd3 = rd2; rd2 = rd1; rd1 = rd0; rd0 = t; }
     }
     FI void encode_match(int32_t backp, uint32_t len, uint32_t ps) {
-        rc_bit(probs + P_IS_REP, state, 0);
+        rc_bit(probs + E_IS_REP, state, 0);
         state = st_match(state);
         len_encode(0, len - kMatchMinLen, ps);
         uint32_t pos = (uint32_t)(backp - kNumRepDistances);
@@ -824,16 +990,16 @@ struct Enc {
         if (pos < (1u << 11)) slot = c_tab.fastpos[pos];
         else if (pos < (1u << 21)) slot = c_tab.fastpos[pos >> 10] + 20;
         else slot = c_tab.fastpos[pos >> 20] + 40;
-        bt_enc(probs + P_POS_SLOT + (len_to_pos_state(len) << 6), kNumPosSlotBits, slot);
+        bt_enc(probs + E_PSLOT + (len_to_pos_state(len) << 6), kNumPosSlotBits, slot);
         if (slot >= (uint32_t)kStartPosModelIndex) {
             uint32_t footer = (slot >> 1) - 1, base = (2 | (slot & 1)) << footer, red = pos - base;
             if (slot < (uint32_t)kEndPosModelIndex) {
-                uint16_t* m = probs + P_POS_ENC + (int32_t)(base - slot - 1);
+                uint16_t* m = probs + E_PENC + (int32_t)(base - slot - 1);
                 uint32_t mm = 1, sym = red;
                 for (uint32_t i = 0; i < footer; i++) { uint32_t bit = sym & 1; rc_bit(m, mm, bit); mm = (mm << 1) | bit; sym >>= 1; }
             } else {
                 rc_direct(red >> kNumAlignBits, (int)(footer - kNumAlignBits));
-                bt_rev_enc(probs + P_ALIGN, kNumAlignBits, red & kAlignMask);
+                bt_rev_enc(probs + E_ALIGN, kNumAlignBits, red & kAlignMask);
                 align_price_count++;
             }
         }
@@ -843,16 +1009,17 @@ struct Enc {
     FI void flush(uint32_t now_pos) {
         if (eos) {   // WriteEndMarker (Encoder.java:818-835)
             uint32_t ps = now_pos & ps_mask;
-            rc_bit(probs + P_IS_MATCH, (state << 4) + ps, 1);
-            rc_bit(probs + P_IS_REP, state, 0);
+            rc_bit(probs + E_IS_MATCH, (state << PBS) + ps, 1);
+            rc_bit(probs + E_IS_REP, state, 0);
             state = st_match(state);
             len_encode(0, 0, ps);
-            bt_enc(probs + P_POS_SLOT + (len_to_pos_state(kMatchMinLen) << 6), kNumPosSlotBits, 63);
+            bt_enc(probs + E_PSLOT + (len_to_pos_state(kMatchMinLen) << 6), kNumPosSlotBits, 63);
             uint32_t red = (1u << 30) - 1;
             rc_direct(red >> kNumAlignBits, 30 - kNumAlignBits);
-            bt_rev_enc(probs + P_ALIGN, kNumAlignBits, red & kAlignMask);
+            bt_rev_enc(probs + E_ALIGN, kNumAlignBits, red & kAlignMask);
         }
         for (int i = 0; i < 5; i++) shift_low();
+        flush_out(outpos & ~(uint64_t)(kObuf - 1), (uint32_t)(outpos & (kObuf - 1)));
     }
 
     FI void run() {   // Encoder.Code: SetStreams + CodeOneBlock/encodeOne (Encoder.java:843-936, 1046-1077)
@@ -860,7 +1027,7 @@ struct Enc {
         for (int k = 0; k < kProfSlots; k++) prof[k] = 0;
 #endif
         const uint32_t nlit = 0x300u << (lc + lp);
-        for (uint32_t i = lane; i < (uint32_t)P_FIXED_COUNT; i += kWave) probs[i] = kBitModelTotal >> 1;
+        for (uint32_t i = lane; i < (uint32_t)E_COUNT; i += kWave) probs[i] = kBitModelTotal >> 1;
         for (uint32_t i = lane; i < nlit; i += kWave) lit[i] = kBitModelTotal >> 1;
         for (uint32_t i = lane; i < 256; i += kWave) psp[i] = 0;
         if (!LIT_LDS) SPILL_FENCE();
@@ -886,11 +1053,11 @@ struct Enc {
         if (avail() == 0) { flush(0); return; }
         read_match_distances();
         DBG(1, 5);
-        rc_bit(probs + P_IS_MATCH, (state << 4) + (now_pos & ps_mask), 0);
+        rc_bit(probs + E_IS_MATCH, (state << PBS) + (now_pos & ps_mask), 0);
         state = st_lit(state);
         {
             uint32_t cb = byte_at(0 - additional_offset);
-            lit_encode(lit_coder(now_pos, prev_byte), cb);
+            lit_encode(lit_coder(now_pos, prev_byte), false, 0, cb);
             prev_byte = cb;
         }
         additional_offset--;
@@ -911,20 +1078,22 @@ struct Enc {
             if (bad || len == 0 || now_pos + len > n) { if (!bad) bad = 5; return; }
             PBEGIN(te);
             uint32_t ps = now_pos & ps_mask;
-            uint32_t cs = (state << 4) + ps;
+            uint32_t cs = (state << PBS) + ps;
             if (len == 1 && back == -1) {
-                rc_bit(probs + P_IS_MATCH, cs, 0);
-                uint32_t cb = byte_at(0 - additional_offset);
+                // both loads issued before the coder work (one round trip; out-of-range reads are 0)
+                const uint32_t cb = byte_at(0 - additional_offset);
+                const uint32_t mb = byte_at((int32_t)(0 - rd0 - 1) - additional_offset);
+                rc_bit(probs + E_IS_MATCH, cs, 0);
                 uint16_t* sub = lit_coder(now_pos, prev_byte);
-                if (st_is_char(state)) lit_encode(sub, cb);
-                else lit_encode_matched(sub, byte_at((int32_t)(0 - rd0 - 1) - additional_offset), cb);
+                lit_encode(sub, !st_is_char(state), mb, cb);
                 prev_byte = cb;
                 state = st_lit(state);
             } else {
-                rc_bit(probs + P_IS_MATCH, cs, 1);
+                const uint32_t last = byte_at((int32_t)len - 1 - additional_offset);
+                rc_bit(probs + E_IS_MATCH, cs, 1);
                 if (back < kNumRepDistances) encode_rep(back, len, ps, cs);
                 else encode_match(back, len, ps);
-                prev_byte = byte_at((int32_t)len - 1 - additional_offset);
+                prev_byte = last;
             }
             additional_offset -= (int32_t)len;
             now_pos += len;
@@ -940,37 +1109,55 @@ struct Enc {
     }
 };
 
-template <typename PairT, bool LIT_LDS>
+// LDS layout of one stream's workgroup; shared by the kernel (carving) and
+// the host (dynamic LDS size). Regions are 16-byte aligned.
+enum { L_PP, L_PROBS, L_LENP, L_LENC, L_PSP, L_DP, L_AP, L_TP, L_MDLEN, L_MDDIST, L_RINFO, L_RPAIRS, L_OPRICE,
+       L_OPP, L_OBP, L_OBP2, L_OFS, L_OBACKS, L_WIN, L_OBUF, L_LIT, L_COUNT };
+__host__ __device__ inline uint32_t enc_lds_layout(const EncArgs& a, uint32_t* off) {
+    const uint32_t md_cap = a.fb + 2;   // pairs per position <= fb (+1 clamp slot)
+    const uint32_t sz[L_COUNT] = {
+        512 * 2, enc_prob_count(a.pb) * 2, 2 * (1u << a.pb) * a.len_table_size * 2, 2 * 16 * 4, 256 * 2, 512 * 2, 16 * 4,
+        kNumFullDistances * 2, md_cap * 2, md_cap * 4, kRing * 4, kRing * kInlinePairs * a.pair_bytes, kOptLds * 4, kOptLds * 4,
+        kOptLds * 4, kOptLds * 4, kOptLds, 4 * kOptLds * 4, kSides * kGW, kObuf,
+        a.lit_in_lds ? (0x300u << (a.lc + a.lp)) * 2 : 0u};
+    uint32_t o = 0;
+    for (int i = 0; i < L_COUNT; i++) { if (off) off[i] = o; o += (sz[i] + 15) & ~15u; }
+    return o;
+}
+
+template <typename PairT, bool LIT_LDS, int PBS>
 __global__ void __launch_bounds__(kWave) enc_kernel(EncArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    Enc<PairT, LIT_LDS> e;
+    Enc<PairT, LIT_LDS, PBS> e;
     e.lane = threadIdx.x;
     e.fb = a.fb; e.lc = a.lc; e.lp = a.lp; e.pb = a.pb; e.ps_mask = (1u << a.pb) - 1; e.eos = a.eos;
     e.dist_table_size = a.dist_table_size; e.tsize = a.len_table_size;
-    size_t off = 0;
-    auto take = [&](size_t bytes) { uint8_t* p = smem + off; off += (bytes + 15) & ~(size_t)15; return p; };
-    e.pp = (uint16_t*)take(512 * 2);
-    e.probs = (uint16_t*)take(P_FIXED_COUNT * 2);
-    e.lenp = (uint16_t*)take((size_t)2 * (1u << a.pb) * a.len_table_size * 2);
-    e.lenc = (uint32_t*)take(2 * 16 * 4);
-    e.psp = (uint32_t*)take(256 * 4);
-    e.dp = (uint32_t*)take(512 * 4);
-    e.ap = (uint32_t*)take(16 * 4);
-    e.tp = (uint32_t*)take(kNumFullDistances * 4);
-    e.md_len = (uint16_t*)take(kMdCap * 2);
-    e.md_dist = (uint32_t*)take(kMdCap * 4);
-    e.ring_info = (uint32_t*)take(kRing * 4);
-    e.ring_pairs = (PairT*)take(kRing * kInlinePairs * 8);
-    e.o_price = (uint32_t*)take(kOptLds * 4);
-    e.o_pp = (uint32_t*)take(kOptLds * 4);
-    e.o_bp = (int32_t*)take(kOptLds * 4);
-    e.o_bp2 = (int32_t*)take(kOptLds * 4);
-    e.o_fs = (uint8_t*)take(kOptLds);
-    e.o_backs = (uint32_t*)take(4 * kOptLds * 4);
+    uint32_t off[L_COUNT];
+    enc_lds_layout(a, off);
+    e.pp = (uint16_t*)(smem + off[L_PP]);
+    e.probs = (uint16_t*)(smem + off[L_PROBS]);
+    e.lenp = (uint16_t*)(smem + off[L_LENP]);
+    e.lenc = (uint32_t*)(smem + off[L_LENC]);
+    e.psp = (uint16_t*)(smem + off[L_PSP]);
+    e.dp = (uint16_t*)(smem + off[L_DP]);
+    e.ap = (uint32_t*)(smem + off[L_AP]);
+    e.tp = (uint16_t*)(smem + off[L_TP]);
+    e.md_len = (uint16_t*)(smem + off[L_MDLEN]);
+    e.md_dist = (uint32_t*)(smem + off[L_MDDIST]);
+    e.ring_info = (uint32_t*)(smem + off[L_RINFO]);
+    e.ring_pairs = (PairT*)(smem + off[L_RPAIRS]);
+    e.o_price = (uint32_t*)(smem + off[L_OPRICE]);
+    e.o_pp = (uint32_t*)(smem + off[L_OPP]);
+    e.o_bp = (int32_t*)(smem + off[L_OBP]);
+    e.o_bp2 = (int32_t*)(smem + off[L_OBP2]);
+    e.o_fs = smem + off[L_OFS];
+    e.o_backs = (uint32_t*)(smem + off[L_OBACKS]);
+    e.win = smem + off[L_WIN];
+    e.obuf = smem + off[L_OBUF];
     uint8_t* scratch = a.scratch + (size_t)blockIdx.x * a.scratch_stride;
     e.spill = __builtin_amdgcn_make_buffer_rsrc(scratch, 0, kNumOpts * 4 * 9, 0x00020000);
     uint16_t* lit_g = (uint16_t*)(scratch + kNumOpts * 4 * 9);
-    if (LIT_LDS) e.lit = (uint16_t*)take((0x300u << (a.lc + a.lp)) * 2);
+    if (LIT_LDS) e.lit = (uint16_t*)(smem + off[L_LIT]);
     else e.lit = lit_g;
     for (int i = (int)e.lane; i < 512; i += kWave) e.pp[i] = (uint16_t)c_tab.prices[i];
     LANE_FENCE();
@@ -983,13 +1170,16 @@ __global__ void __launch_bounds__(kWave) enc_kernel(EncArgs a) {
     // One workgroup per stream, longest first (order[]): the dispatcher is the
     // work queue, so the kernel has no outer loop and every wave retires at
     // the end of its stream.
-    const int s = (int)a.order[blockIdx.x];
-    e.gbase = a.offs[s];
-    e.n = (uint32_t)(a.offs[s + 1] - e.gbase);
+    // wave-uniform by construction; readfirstlane keeps them (and the buffer
+    // descriptor built from them) in SGPRs, so buffer loads need no waterfall loop
+    const int s = __builtin_amdgcn_readfirstlane((int)a.order[blockIdx.x]);
+    e.gbase = uni64(a.offs[s]);
+    e.n = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(uni64(a.offs[s + 1]) - e.gbase));
     e.in = a.in + e.gbase;
     e.inb = __builtin_amdgcn_make_buffer_rsrc((void*)e.in, 0, e.n, 0x00020000);
-    e.out = a.out + a.out_offs[s];
-    e.cap = a.out_offs[s + 1] - a.out_offs[s];
+    const uint64_t oo = uni64(a.out_offs[s]);
+    e.out = a.out + oo;
+    e.cap = uni64(a.out_offs[s + 1]) - oo;
     if (e.dbg && e.lane == 0) __hip_atomic_store(e.dbg + 8, (uint32_t)s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 #ifdef LZG_PROF
     const uint64_t t_run = __builtin_amdgcn_s_memtime();
@@ -1006,14 +1196,7 @@ __global__ void __launch_bounds__(kWave) enc_kernel(EncArgs a) {
     }
 }
 
-size_t enc_lds_bytes(const EncArgs& a) {
-    auto r = [](size_t b) { return (b + 15) & ~(size_t)15; };
-    size_t s = r(512 * 2) + r(P_FIXED_COUNT * 2) + r((size_t)2 * (1u << a.pb) * a.len_table_size * 2) + r(2 * 16 * 4) +
-               r(256 * 4) + r(512 * 4) + r(16 * 4) + r(kNumFullDistances * 4) + r(kMdCap * 2) + r(kMdCap * 4) +
-               r(kRing * 4) + r(kRing * kInlinePairs * 8) + 4 * r(kOptLds * 4) + r(kOptLds) + r(4 * kOptLds * 4);
-    if (a.lit_in_lds) s += r((0x300u << (a.lc + a.lp)) * 2);
-    return s;
-}
+size_t enc_lds_bytes(const EncArgs& a) { return enc_lds_layout(a, nullptr); }
 
 size_t enc_scratch_per_block(const Derived& d) {
     return (size_t)kNumOpts * 4 * 9 + ((size_t)0x300 << (d.lc + d.lp)) * 2 + 256;
@@ -1023,23 +1206,30 @@ uint32_t enc_lit_in_lds(const Derived& d) { return (d.lc + d.lp) <= (uint32_t)kL
 
 int enc_grid(const Derived&, int nstreams) { return nstreams; }   // one workgroup per stream
 
-template <typename PairT, bool LIT>
+template <typename PairT, bool LIT, int PBS>
 static void launch_one(Ctx* ctx, const EncArgs& a, int grid, size_t lds, hipStream_t st) {
     if (lds > 64 * 1024)
-        hipFuncSetAttribute((const void*)enc_kernel<PairT, LIT>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        hipFuncSetAttribute((const void*)enc_kernel<PairT, LIT, PBS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     TimedLaunch tl(ctx, "enc_parse", st);
-    hipLaunchKernelGGL((enc_kernel<PairT, LIT>), dim3(grid), dim3(kWave), lds, st, a);
+    hipLaunchKernelGGL((enc_kernel<PairT, LIT, PBS>), dim3(grid), dim3(kWave), lds, st, a);
+}
+
+template <typename PairT, bool LIT>
+static void launch_pb(Ctx* ctx, const EncArgs& a, int grid, size_t lds, hipStream_t st) {
+    if (a.pb <= 2) launch_one<PairT, LIT, 2>(ctx, a, grid, lds, st);
+    else launch_one<PairT, LIT, 4>(ctx, a, grid, lds, st);
 }
 
 int launch_encoder(Ctx* ctx, const EncArgs& a, bool wide_pairs, int grid, hipStream_t st) {
+    if (a.pair_bytes != (wide_pairs ? 8u : 4u)) return ctx->fail(LZMA_E_INTERNAL, "pair width mismatch");
     size_t lds = enc_lds_bytes(a);
     if (lds > 160 * 1024) return ctx->fail(LZMA_E_PARAM, "encoder LDS %zu too large", lds);
     if (wide_pairs) {
-        if (a.lit_in_lds) launch_one<uint64_t, true>(ctx, a, grid, lds, st);
-        else launch_one<uint64_t, false>(ctx, a, grid, lds, st);
+        if (a.lit_in_lds) launch_pb<uint64_t, true>(ctx, a, grid, lds, st);
+        else launch_pb<uint64_t, false>(ctx, a, grid, lds, st);
     } else {
-        if (a.lit_in_lds) launch_one<uint32_t, true>(ctx, a, grid, lds, st);
-        else launch_one<uint32_t, false>(ctx, a, grid, lds, st);
+        if (a.lit_in_lds) launch_pb<uint32_t, true>(ctx, a, grid, lds, st);
+        else launch_pb<uint32_t, false>(ctx, a, grid, lds, st);
     }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return ctx->fail(LZMA_E_DEVICE, "enc launch: %s", hipGetErrorString(e));

@@ -213,6 +213,7 @@ struct EncArgs {
     uint64_t scratch_stride;
     uint32_t fb, lc, lp, pb, eos, dist_table_size, len_table_size;
     uint32_t lit_in_lds;
+    uint32_t pair_bytes;          // 4 (u32 packed pairs) or 8 (u64, streams >= 8 MiB)
     uint32_t* dbg;                // debug checkpoints (host-mapped, LZMA_MI355X_DEBUG only) or null
     uint64_t* prof;               // phase cycles [nstreams][kProfSlots] (LZG_PROF builds) or null
 };

@@ -208,6 +208,9 @@ inline unsigned long long __ballot(int pred) {
     return m;
 }
 #define __builtin_amdgcn_fence(order, scope) __atomic_signal_fence(__ATOMIC_SEQ_CST)
+// wave width 1: the first active lane is the only lane
+inline int __builtin_amdgcn_readfirstlane(int v) { return v; }
+inline int __builtin_amdgcn_readlane(int v, int) { return v; }
 #define __builtin_nontemporal_load(p) (*(p))
 #define __builtin_nontemporal_store(v, p) (*(p) = (v))
 struct __amdgpu_buffer_rsrc_t { uint8_t* base; uint32_t bytes; };
