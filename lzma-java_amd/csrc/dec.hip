@@ -1,36 +1,87 @@
 // dec.hip -- batched LZMA decoder: src/main/java/SevenZip/Compression/LZMA/
 // Decoder.java (Code :205-301) with RangeDecoder.java and OutWindow.java, one
-// wavefront (kWave = 64 lanes) per independent stream pulled from a work queue.
+// wavefront (kWave = 64 lanes) per independent stream, one workgroup per
+// stream (longest first).
 //
-// The DecodeBit chain is strictly serial, so it runs as wave-uniform code;
-// the probability models live in LDS. The output buffer in HBM is the window
-// (OutWindow's ring is unobservable when the whole output is resident), and
-// long match copies (OutWindow.CopyBlock, OutWindow.java:53-67) use all
-// lanes when the source lies wholly before the destination.
+// The DecodeBit chain is strictly serial, so it runs as wave-uniform scalar
+// code; the probability models live in LDS. Memory round trips are kept off
+// that chain:
+//   * compressed input is staged through an LDS ring (kIbuf bytes, refilled
+//     by all lanes at once), so RangeDecoder's byte reads are LDS reads;
+//   * the most recent kWin output bytes live in an LDS window (OutWindow,
+//     OutWindow.java:15-82); match copies and matched-literal bytes read it,
+//     with all lanes copying (an overlapping copy repeats the d-byte period:
+//     out[now + k] = out[now - d + k % d]);
+//   * the window is flushed to HBM kFlush bytes at a time (coalesced); a
+//     distance beyond half the window reads the flushed bytes in HBM.
 #include "lzma_common.h"
 #include "runtime.h"
 
 namespace lzg {
 
 constexpr int kDecLitLdsMaxBits = 3;
+constexpr uint32_t kIbuf = 256;     // input staging ring
+constexpr uint32_t kWin = 2048;     // output window in LDS (power of two)
+constexpr uint32_t kFlush = 256;    // window -> HBM flush granule
+constexpr uint32_t kNear = kWin / 2;   // distances <= kNear read the LDS window
+static_assert(kFlush + kMatchMaxLen + 64 <= kNear, "window too small for the flush lag");
 
-#define WSYNC() __syncthreads()
+#define DFI __device__ __forceinline__
+#define LANE_FENCE() asm volatile("" ::: "memory")
+
+DFI uint64_t dec_uni64(uint64_t v) {
+    return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32)) << 32) |
+           (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+}
 
 struct Dec {
-    int lane;
+    uint32_t lane;
     uint16_t* probs;
     uint16_t* lit;
+    uint8_t* ibuf;                // [kIbuf]
+    uint8_t* win;                 // [kWin]
     uint32_t lc, lp, pb, ps_mask, dict_check;
     const uint8_t* in;
-    uint64_t n_in, ipos;
+    uint64_t n_in, ipos, ibase;
     uint8_t* out;
-    uint64_t cap;
+    uint64_t cap, flushed;
     uint32_t range, code;
 
-    __device__ uint32_t rd_byte() {   // InputStream.read(): -1 past the end
-        return ipos < n_in ? (uint32_t)in[ipos++] : 0xFFFFFFFFu;
+    // ---- input (InputStream.read(): -1 past the end)
+    DFI void refill(uint64_t base) {
+        ibase = base;
+        for (uint32_t k = lane; k < kIbuf; k += kWave) {
+            const uint64_t q = base + k;
+            ibuf[k] = q < n_in ? in[q] : 0;
+        }
+        LANE_FENCE();
     }
-    __device__ uint32_t bit(uint16_t* p, uint32_t idx) {   // RangeDecoder.DecodeBit (RangeDecoder.java:43-64)
+    DFI uint32_t rd_byte() {
+        if (ipos >= n_in) return 0xFFFFFFFFu;
+        if (ipos - ibase >= kIbuf) refill(ipos);
+        return (uint32_t)ibuf[(uint32_t)(ipos++ - ibase)];
+    }
+    // ---- output window
+    DFI void flush_to(uint64_t upto) {   // write [flushed, upto) to HBM (upto <= now, within the window)
+        LANE_FENCE();
+        for (uint64_t k = flushed + lane; k < upto; k += kWave) out[k] = win[(uint32_t)k & (kWin - 1)];
+        flushed = upto;
+        LANE_FENCE();
+    }
+    DFI void maybe_flush(uint64_t now) {
+        if (now - flushed >= kFlush) flush_to(now & ~(uint64_t)(kFlush - 1));
+    }
+    DFI uint32_t byte_back(uint64_t now, uint32_t d1) {   // out[now - d1], 1 <= d1 <= now
+        if (d1 <= kNear) return win[(uint32_t)(now - d1) & (kWin - 1)];
+        return out[now - d1];                              // flushed long ago (d1 > kNear > lag)
+    }
+    DFI void put(uint64_t now, uint32_t b) {
+        if (lane == 0) win[(uint32_t)now & (kWin - 1)] = (uint8_t)b;
+        LANE_FENCE();
+    }
+
+    // ---- range decoder
+    DFI uint32_t bit(uint16_t* p, uint32_t idx) {   // RangeDecoder.DecodeBit (RangeDecoder.java:43-64)
         uint32_t prob = p[idx];
         uint32_t bound = (range >> 11) * prob;
         uint32_t r;
@@ -47,7 +98,7 @@ struct Dec {
         if ((range & kTopMask) == 0) { code = (code << 8) | rd_byte(); range <<= 8; }
         return r;
     }
-    __device__ uint32_t direct(int nbits) {   // RangeDecoder.DecodeDirectBits (RangeDecoder.java:27-41)
+    DFI uint32_t direct(int nbits) {   // RangeDecoder.DecodeDirectBits (RangeDecoder.java:27-41)
         uint32_t result = 0;
         for (int i = nbits; i != 0; i--) {
             range >>= 1;
@@ -58,31 +109,49 @@ struct Dec {
         }
         return result;
     }
-    __device__ uint32_t bt_dec(uint16_t* p, int nbits) {   // BitTreeDecoder.Decode
+    DFI uint32_t bt_dec(uint16_t* p, int nbits) {   // BitTreeDecoder.Decode (BitTreeDecoder.java:19-25)
         uint32_t m = 1;
         for (int b = nbits; b != 0; b--) m = (m << 1) + bit(p, m);
         return m - (1u << nbits);
     }
-    __device__ uint32_t bt_rev_dec(uint16_t* p, int nbits) {   // BitTreeDecoder.ReverseDecode / Decoder.ReverseDecode
+    DFI uint32_t bt_rev_dec(uint16_t* p, int nbits) {   // BitTreeDecoder.ReverseDecode (:27-37)
         uint32_t m = 1, sym = 0;
         for (int b = 0; b < nbits; b++) { uint32_t x = bit(p, m); m <<= 1; m += x; sym |= x << b; }
         return sym;
     }
-    __device__ uint32_t len_dec(uint16_t* L, uint32_t ps) {   // Decoder.LenDecoder.Decode (Decoder.java:48-59)
+    DFI uint32_t len_dec(uint16_t* L, uint32_t ps) {   // Decoder.LenDecoder.Decode (Decoder.java:48-59)
         if (bit(L, LEN_CHOICE) == 0) return bt_dec(L + LEN_LOW + ps * 8, 3);
         uint32_t sym = kNumLowLenSymbols;
         if (bit(L, LEN_CHOICE + 1) == 0) sym += bt_dec(L + LEN_MID + ps * 8, 3);
         else sym += kNumMidLenSymbols + bt_dec(L + LEN_HIGH, 8);
         return sym;
     }
+    // OutWindow.CopyBlock (OutWindow.java:53-67) of len bytes at distance d1,
+    // byte-serial semantics: an overlapping copy repeats the d1-byte period.
+    DFI void copy(uint64_t now, uint32_t d1, uint32_t len) {
+        LANE_FENCE();
+        for (uint32_t k0 = 0; k0 < len; k0 += kWave) {
+            const uint32_t k = k0 + lane;
+            if (k < len) {
+                // source = now - d1 + (k mod d1): always before `now`, so lanes never
+                // read a byte this copy writes (and kNear + 273 < kWin: no ring alias)
+                const uint32_t r = k % d1;
+                win[(uint32_t)(now + k) & (kWin - 1)] = (uint8_t)byte_back(now, d1 - r);
+            }
+        }
+        LANE_FENCE();
+    }
 
-    // returns LZMA_OK / LZMA_E_DATA / LZMA_E_OVERFLOW; *now = bytes written
-    __device__ int run(int64_t out_size, uint64_t* now_out) {
+    // returns LZMA_OK / LZMA_E_DATA / LZMA_E_OVERFLOW; *now_out = bytes written
+    DFI int run(int64_t out_size, uint64_t* now_out) {
         const uint32_t nlit = 0x300u << (lc + lp);
         for (uint32_t i = lane; i < (uint32_t)P_FIXED_COUNT; i += kWave) probs[i] = kBitModelTotal >> 1;
         for (uint32_t i = lane; i < nlit; i += kWave) lit[i] = kBitModelTotal >> 1;
-        WSYNC();
+        LANE_FENCE();
         ipos = 0;
+        ibase = 0;
+        refill(0);
+        flushed = 0;
         code = 0;
         range = 0xFFFFFFFFu;
         for (int i = 0; i < 5; i++) code = (code << 8) | rd_byte();   // RangeDecoder.Init
@@ -91,14 +160,14 @@ struct Dec {
         uint32_t prev = 0;
         int rc = LZMA_OK;
         while (out_size < 0 || (int64_t)now < out_size) {
-            uint32_t ps = (uint32_t)now & ps_mask;
+            const uint32_t ps = (uint32_t)now & ps_mask;
             if (bit(probs + P_IS_MATCH, (state << 4) + ps) == 0) {
                 uint16_t* sub = lit + (size_t)((((uint32_t)now & ((1u << lp) - 1)) << lc) + (prev >> (8 - lc))) * 0x300;
                 uint32_t sym = 1;
                 if (st_is_char(state)) {
                     do { sym = (sym << 1) | bit(sub, sym); } while (sym < 0x100);
-                } else {
-                    uint32_t mb = out[now - rep0 - 1];
+                } else {   // LiteralDecoder.Decoder2.DecodeWithMatchByte (Decoder.java:80-102)
+                    uint32_t mb = byte_back(now, rep0 + 1);
                     do {
                         uint32_t mbit = (mb >> 7) & 1;
                         mb <<= 1;
@@ -112,7 +181,7 @@ struct Dec {
                 }
                 prev = sym & 0xFF;
                 if (now >= cap) { rc = LZMA_E_OVERFLOW; break; }
-                out[now] = (uint8_t)prev;
+                put(now, prev);
                 now++;
                 state = st_lit(state);
             } else {
@@ -157,25 +226,21 @@ struct Dec {
                     }
                 }
                 if ((uint64_t)rep0 >= now || rep0 >= dict_check) { rc = LZMA_E_DATA; break; }
-                // OutWindow.CopyBlock: byte-serial semantics (overlapping copies repeat the pattern)
-                uint64_t d1 = (uint64_t)rep0 + 1;
+                const uint32_t d1 = rep0 + 1;
                 if (now + len > cap) {   // copy what fits, then report (no bytes past the capacity)
-                    for (uint64_t k = 0; now + k < cap; k++) out[now + k] = out[now + k - d1];
+                    const uint32_t fit = (uint32_t)(cap - now);
+                    copy(now, d1, fit);
                     now = cap;
                     rc = LZMA_E_OVERFLOW;
                     break;
                 }
-                if (d1 >= len && len >= 32) {   // source fully written before the copy starts
-                    WSYNC();
-                    for (uint32_t k = lane; k < len; k += kWave) out[now + k] = out[now + k - d1];
-                    WSYNC();
-                } else {
-                    for (uint32_t k = 0; k < len; k++) out[now + k] = out[now + k - d1];
-                }
+                copy(now, d1, len);
                 now += len;
-                prev = out[now - 1];
+                prev = win[(uint32_t)(now - 1) & (kWin - 1)];
             }
+            maybe_flush(now);
         }
+        flush_to(now);
         *now_out = now;
         return rc;
     }
@@ -186,53 +251,40 @@ __global__ void __launch_bounds__(kWave) dec_kernel(DecArgs a) {
     Dec d;
     d.lane = threadIdx.x;
     d.lc = a.lc; d.lp = a.lp; d.pb = a.pb; d.ps_mask = (1u << a.pb) - 1; d.dict_check = a.dict_check;
-    d.probs = (uint16_t*)smem;
-    size_t off = ((size_t)P_FIXED_COUNT * 2 + 15) & ~(size_t)15;
-    if (a.lit_in_lds) d.lit = (uint16_t*)(smem + off);
-    else d.lit = (uint16_t*)(a.scratch + blockIdx.x * a.scratch_stride);
-    for (;;) {
-        int idx = 0;
-        if (d.lane == 0) idx = (int)atomicAdd(a.next, 1u);
-        idx = __shfl(idx, 0);
-        if (idx >= a.nstreams) break;
-        int s = (int)a.order[idx];
-        d.in = a.in + a.in_offs[s];
-        d.n_in = a.in_offs[s + 1] - a.in_offs[s];
-        d.out = a.out + a.out_offs[s];
-        d.cap = a.out_offs[s + 1] - a.out_offs[s];
-        uint64_t now = 0;
-        int rc = d.run(a.out_sizes[s], &now);
-        if (d.lane == 0) { a.out_lens[s] = now; a.status[s] = rc; }
-        WSYNC();
-    }
+    size_t off = 0;
+    auto take = [&](size_t bytes) { uint8_t* p = smem + off; off += (bytes + 15) & ~(size_t)15; return p; };
+    d.probs = (uint16_t*)take((size_t)P_FIXED_COUNT * 2);
+    d.ibuf = take(kIbuf);
+    d.win = take(kWin);
+    if (a.lit_in_lds) d.lit = (uint16_t*)take(((size_t)0x300 << (a.lc + a.lp)) * 2);
+    else d.lit = (uint16_t*)(a.scratch + (size_t)blockIdx.x * a.scratch_stride);
+    // one workgroup per stream; per-stream values are wave-uniform (readfirstlane keeps them scalar)
+    const int s = __builtin_amdgcn_readfirstlane((int)a.order[blockIdx.x]);
+    const uint64_t i0 = dec_uni64(a.in_offs[s]), o0 = dec_uni64(a.out_offs[s]);
+    d.in = a.in + i0;
+    d.n_in = dec_uni64(a.in_offs[s + 1]) - i0;
+    d.out = a.out + o0;
+    d.cap = dec_uni64(a.out_offs[s + 1]) - o0;
+    const int64_t out_size = (int64_t)dec_uni64((uint64_t)a.out_sizes[s]);
+    uint64_t now = 0;
+    int rc = d.run(out_size, &now);
+    if (d.lane == 0) { a.out_lens[s] = now; a.status[s] = rc; }
 }
 
 size_t dec_scratch_per_block(uint32_t lc, uint32_t lp) { return ((size_t)0x300 << (lc + lp)) * 2 + 256; }
 
 static size_t dec_lds_bytes(uint32_t lc, uint32_t lp, uint32_t lit_in_lds) {
-    size_t lds = ((size_t)P_FIXED_COUNT * 2 + 15) & ~(size_t)15;
-    if (lit_in_lds) lds += ((size_t)0x300 << (lc + lp)) * 2;
+    auto r = [](size_t b) { return (b + 15) & ~(size_t)15; };
+    size_t lds = r((size_t)P_FIXED_COUNT * 2) + r(kIbuf) + r(kWin);
+    if (lit_in_lds) lds += r(((size_t)0x300 << (lc + lp)) * 2);
     return lds;
 }
 
-int dec_grid(uint32_t lc, uint32_t lp, uint32_t lit_in_lds, int nstreams) {
-    size_t lds = dec_lds_bytes(lc, lp, lit_in_lds);
-    int dev = 0;
-    hipGetDevice(&dev);
-    int cus = 0;
-    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (cus <= 0) cus = 256;
-    int per_cu = (int)((160 * 1024) / (lds + 256));
-    if (per_cu > 16) per_cu = 16;
-    if (per_cu < 1) per_cu = 1;
-    int grid = cus * per_cu;
-    if (grid > nstreams) grid = nstreams;
-    if (grid < 1) grid = 1;
-    return grid;
-}
+int dec_grid(uint32_t, uint32_t, uint32_t, int nstreams) { return nstreams; }   // one workgroup per stream
 
 int launch_decoder(Ctx* ctx, const DecArgs& a, int grid, hipStream_t st) {
     size_t lds = dec_lds_bytes(a.lc, a.lp, a.lit_in_lds);
+    if (lds > 64 * 1024) hipFuncSetAttribute((const void*)dec_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     TimedLaunch tl(ctx, "dec_stream", st);
     hipLaunchKernelGGL(dec_kernel, dim3(grid), dim3(kWave), lds, st, a);
     hipError_t e = hipGetLastError();

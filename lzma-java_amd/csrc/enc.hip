@@ -51,7 +51,14 @@ constexpr int kLitSlots = (8 + kWave - 1) / kWave;   // literal bits per lane (1
 #define SPILL_FENCE() __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup")
 // every loop spends from one per-stream budget; exhausting it records the loop id
 // debug checkpoint (block 0, lane 0) into host-mapped memory
+// (LZG_DEBUG builds only)
+#ifdef LZG_DEBUG
 #define DBG(k, v) do { if (dbg && blockIdx.x == 0 && lane == 0) __hip_atomic_store(dbg + (k), (uint32_t)(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); } while (0)
+#else
+#define DBG(k, v) do {} while (0)
+#endif
+// The two unbounded-looking loops (the per-call parse loop and the per-symbol
+// coding loop) spend from one budget; the inner loops are bounded by design.
 #define WDOG(id) if (++wd > wd_max) { bad = 100 + (id); break; }
 // Phase profile (profiling build only, -DLZG_PROF): s_memtime cycles per phase,
 // summed per stream into EncArgs::prof[stream * kProfSlots + phase].
@@ -142,10 +149,10 @@ struct Enc {
     __amdgpu_buffer_rsrc_t inb;   // the stream's bytes, range-checked (out of range reads 0, never fault)
     uint32_t n;
     uint32_t bad;                 // internal-consistency watchdog tripped (reason code, 0 = fine)
-    uint64_t wd, wd_max;          // loop-iteration watchdog (budget per stream)
+    uint32_t wd, wd_max;          // loop-iteration watchdog (budget per stream)
     uint32_t* dbg;
     uint8_t* out;
-    uint64_t cap, outpos;
+    uint32_t cap, outpos;      // streams < 2 GiB: outputs < 4 GiB
     uint32_t overflow;
     const uint32_t* minfo;
     const PairT* pairs;
@@ -260,7 +267,6 @@ struct Enc {
         if (limit <= 0) return 0;
         const uint32_t a = (uint32_t)p0, b = (uint32_t)p0 - (distance + 1);
         for (int32_t i0 = 0; i0 < limit; i0 += kWave) {
-            WDOG(2);
             int32_t i = i0 + (int32_t)lane;
             bool ne = i < limit ? (in_byte(a + (uint32_t)i) != in_byte(b + (uint32_t)i)) : true;
             uint64_t m = __ballot(ne);
@@ -346,7 +352,7 @@ struct Enc {
     // Output bytes are staged in LDS and written kObuf at a time by all lanes:
     // a global store per byte would make the next dependent load wait for it
     // (vmcnt counts stores and loads alike on CDNA).
-    FI void flush_out(uint64_t start, uint32_t count) {
+    FI void flush_out(uint32_t start, uint32_t count) {
         LANE_FENCE();
         for (uint32_t i = lane; i < count; i += kWave)
             if (start + i < cap) out[start + i] = obuf[i];
@@ -362,7 +368,7 @@ struct Enc {
         uint32_t hi = (uint32_t)(low >> 32);
         if (hi != 0 || low < 0xFF000000ull) {
             uint32_t temp = cache;
-            do { WDOG(1); put_byte((temp + hi) & 0xFF); temp = 0xFF; } while (--cache_size != 0);
+            do { put_byte((temp + hi) & 0xFF); temp = 0xFF; } while (--cache_size != 0);
             cache = ((uint32_t)low) >> 24;
         }
         cache_size++;
@@ -1019,7 +1025,7 @@ struct Enc {
             bt_rev_enc(probs + E_ALIGN, kNumAlignBits, red & kAlignMask);
         }
         for (int i = 0; i < 5; i++) shift_low();
-        flush_out(outpos & ~(uint64_t)(kObuf - 1), (uint32_t)(outpos & (kObuf - 1)));
+        flush_out(outpos & ~(uint32_t)(kObuf - 1), outpos & (kObuf - 1));
     }
 
     FI void run() {   // Encoder.Code: SetStreams + CodeOneBlock/encodeOne (Encoder.java:843-936, 1046-1077)
@@ -1036,7 +1042,7 @@ struct Enc {
         rd0 = rd1 = rd2 = rd3 = 0;
         rp0 = rp1 = rp2 = rp3 = 0;
         low = 0; range = 0xFFFFFFFFu; cache_size = 1; cache = 0; outpos = 0; overflow = 0; bad = 0;
-        wd = 0; wd_max = ((uint64_t)n + 64) * 4096;
+        wd = 0; wd_max = n < 0x50000000u ? 3 * n + 4096 : 0xFFFFFFFFu;   // iterations <= 2n + calls
         longest_found = 0; opt_end = 0; opt_cur = 0; additional_offset = 0;
         longest_len = 0; num_pairs = 0; mfpos = 0;
         ring_base = 0x80000000u;   // force a fill at the first read (streams < 2 GiB)
@@ -1162,7 +1168,9 @@ __global__ void __launch_bounds__(kWave) enc_kernel(EncArgs a) {
     for (int i = (int)e.lane; i < 512; i += kWave) e.pp[i] = (uint16_t)c_tab.prices[i];
     LANE_FENCE();
     e.dbg = a.dbg;
+#ifdef LZG_DEBUG
     if (e.dbg && blockIdx.x == 0 && e.lane == 0) __hip_atomic_store(e.dbg, 7u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+#endif
     e.minfo = a.minfo;
     e.pairs = (const PairT*)a.pairs;
     e.ovf_off = a.ovf_off;
@@ -1179,8 +1187,11 @@ __global__ void __launch_bounds__(kWave) enc_kernel(EncArgs a) {
     e.inb = __builtin_amdgcn_make_buffer_rsrc((void*)e.in, 0, e.n, 0x00020000);
     const uint64_t oo = uni64(a.out_offs[s]);
     e.out = a.out + oo;
-    e.cap = uni64(a.out_offs[s + 1]) - oo;
+    const uint64_t cap64 = uni64(a.out_offs[s + 1]) - oo;
+    e.cap = cap64 > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)cap64;   // any stream's output is < 4 GiB
+#ifdef LZG_DEBUG
     if (e.dbg && e.lane == 0) __hip_atomic_store(e.dbg + 8, (uint32_t)s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+#endif
 #ifdef LZG_PROF
     const uint64_t t_run = __builtin_amdgcn_s_memtime();
 #endif
@@ -1191,7 +1202,7 @@ __global__ void __launch_bounds__(kWave) enc_kernel(EncArgs a) {
         for (int k = 0; k < kProfSlots; k++) a.prof[(size_t)s * kProfSlots + k] = e.prof[k];
 #endif
     if (e.lane == 0) {
-        a.out_lens[s] = e.bad ? (((uint64_t)e.bad << 32) | e.mfpos) : e.outpos;
+        a.out_lens[s] = e.bad ? (((uint64_t)e.bad << 32) | e.mfpos) : (uint64_t)e.outpos;
         a.status[s] = e.bad ? LZMA_E_INTERNAL : (e.overflow ? LZMA_E_OVERFLOW : LZMA_OK);
     }
 }
