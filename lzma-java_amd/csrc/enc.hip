@@ -49,6 +49,11 @@ constexpr int kLitSlots = (8 + kWave - 1) / kWave;   // literal bits per lane (1
 // machine schedulers from moving LDS accesses across an exchange point.
 #define LANE_FENCE() asm volatile("" ::: "memory")
 #define SPILL_FENCE() __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup")
+// `for (v = lo + lane; v < hi; v += kWave)` with a wave-uniform trip count: the
+// loop itself stays a scalar loop (a lane-dependent exit costs exec-mask
+// bookkeeping on every iteration and makes values after it look per-lane).
+#define LANE_FOR(T, v, lo, hi) \
+    for (T v##_0 = (lo); v##_0 < (hi); v##_0 += kWave) if (const T v = v##_0 + (T)lane; v < (hi))
 // every loop spends from one per-stream budget; exhausting it records the loop id
 // debug checkpoint (block 0, lane 0) into host-mapped memory
 // (LZG_DEBUG builds only)
@@ -86,28 +91,6 @@ FI uint32_t lane_value(const uint32_t (&v)[N], int j) {
 
 FI uint32_t sel4(uint32_t i, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
     return i == 0 ? a : (i == 1 ? b : (i == 2 ? c : d));
-}
-
-// Encoder-side probability layout (the models of Encoder.java:113-128). The
-// posState-indexed models (isMatch, isRep0Long, the low/mid length coders) are
-// strided by 1 << PBS posStates: PBS = 2 serves pb <= 2 (the common case, and
-// 1.3 KiB less LDS per stream than the 16-posState layout), PBS = 4 serves pb 3-4.
-template <int PBS>
-struct ProbLayout {
-    static constexpr int IS_MATCH = 0;
-    static constexpr int IS_REP = IS_MATCH + (kNumStates << PBS);
-    static constexpr int G0 = IS_REP + kNumStates, G1 = G0 + kNumStates, G2 = G1 + kNumStates;
-    static constexpr int R0L = G2 + kNumStates;
-    static constexpr int PSLOT = R0L + (kNumStates << PBS);
-    static constexpr int PENC = PSLOT + (kNumLenToPosStates << kNumPosSlotBits);
-    static constexpr int ALIGN = PENC + (kNumFullDistances - kEndPosModelIndex);
-    static constexpr int LOW = 2, MID = LOW + (8 << PBS), HIGH = MID + (8 << PBS), LSIZE = HIGH + 256;
-    static constexpr int LEN = ALIGN + kAlignTableSize;
-    static constexpr int RLEN = LEN + LSIZE;
-    static constexpr int COUNT = RLEN + LSIZE;
-};
-__host__ __device__ inline uint32_t enc_prob_count(uint32_t pb) {
-    return pb <= 2 ? (uint32_t)ProbLayout<2>::COUNT : (uint32_t)ProbLayout<4>::COUNT;
 }
 
 template <typename PairT, bool LIT_LDS, int PBS>
@@ -240,7 +223,7 @@ struct Enc {
             uint32_t diff = (mb ^ sym) & 0xFFu;
             first = diff ? 31 - __clz(diff) : -1;
         }
-        for (int j = (int)lane; j < 8; j += kWave) {
+        LANE_FOR(int, j, 0, 8) {
             int i = 7 - j;
             uint32_t bit = (sym >> i) & 1;
             uint32_t ctx = (0x100u | sym) >> (i + 1);
@@ -354,7 +337,7 @@ struct Enc {
     // (vmcnt counts stores and loads alike on CDNA).
     FI void flush_out(uint32_t start, uint32_t count) {
         LANE_FENCE();
-        for (uint32_t i = lane; i < count; i += kWave)
+        LANE_FOR(uint32_t, i, 0u, count)
             if (start + i < cap) out[start + i] = obuf[i];
         LANE_FENCE();
     }
@@ -446,7 +429,7 @@ struct Enc {
         uint32_t a0 = price0(L[LEN_CHOICE]), a1 = price1(L[LEN_CHOICE]);
         uint32_t b0 = a1 + price0(L[LEN_CHOICE + 1]), b1 = a1 + price1(L[LEN_CHOICE + 1]);
         uint16_t* dst = lenp + (which << pb) * tsize + ps * tsize;
-        for (uint32_t i = lane; i < tsize; i += kWave) {
+        LANE_FOR(uint32_t, i, 0u, tsize) {
             uint32_t pr;
             if (i < (uint32_t)kNumLowLenSymbols) pr = a0 + bt_price(L + E_LOW + ps * 8, 3, i);
             else if (i < (uint32_t)(kNumLowLenSymbols + kNumMidLenSymbols)) pr = b0 + bt_price(L + E_MID + ps * 8, 3, i - kNumLowLenSymbols);
@@ -470,13 +453,13 @@ struct Enc {
         if (c == 0) update_len_table(which, ps);
     }
     FI void fill_distances_prices() {   // Encoder.java:1087-1118
-        for (uint32_t i = kStartPosModelIndex + lane; i < (uint32_t)kNumFullDistances; i += kWave) {
+        LANE_FOR(uint32_t, i, (uint32_t)kStartPosModelIndex, (uint32_t)kNumFullDistances) {
             uint32_t ps = c_tab.fastpos[i], footer = (ps >> 1) - 1, base = (2 | (ps & 1)) << footer;
             tp[i] = (uint16_t)rev_price(probs + E_PENC + (int32_t)(base - ps - 1), (int)footer, i - base);
         }
         for (uint32_t l = 0; l < (uint32_t)kNumLenToPosStates; l++) {
             uint32_t st = l << kNumPosSlotBits;
-            for (uint32_t ps = lane; ps < dist_table_size; ps += kWave) {
+            LANE_FOR(uint32_t, ps, 0u, dist_table_size) {
                 uint32_t pr = bt_price(probs + E_PSLOT + st, kNumPosSlotBits, ps);
                 if (ps >= (uint32_t)kEndPosModelIndex) pr += (((ps >> 1) - 1) - kNumAlignBits) << 6;
                 psp[st + ps] = (uint16_t)pr;
@@ -485,14 +468,14 @@ struct Enc {
         LANE_FENCE();
         for (uint32_t l = 0; l < (uint32_t)kNumLenToPosStates; l++) {
             uint32_t st = l << kNumPosSlotBits, st2 = l * kNumFullDistances;
-            for (uint32_t i = lane; i < (uint32_t)kNumFullDistances; i += kWave)
+            LANE_FOR(uint32_t, i, 0u, (uint32_t)kNumFullDistances)
                 dp[st2 + i] = (uint16_t)(i < (uint32_t)kStartPosModelIndex ? psp[st + i] : psp[st + c_tab.fastpos[i]] + tp[i]);
         }
         match_price_count = 0;
         LANE_FENCE();
     }
     FI void fill_align_prices() {   // Encoder.java:1120-1125
-        for (uint32_t i = lane; i < (uint32_t)kAlignTableSize; i += kWave) ap[i] = rev_price(probs + E_ALIGN, kNumAlignBits, i);
+        LANE_FOR(uint32_t, i, 0u, (uint32_t)kAlignTableSize) ap[i] = rev_price(probs + E_ALIGN, kNumAlignBits, i);
         align_price_count = 0;
         LANE_FENCE();
     }
@@ -500,7 +483,7 @@ struct Enc {
     // ------------------------------------------------------------ match lists (phase 1 output)
     FI void ring_fill(uint32_t base) {
         ring_base = base;
-        for (uint32_t k = lane; k < (uint32_t)kRing; k += kWave) {
+        LANE_FOR(uint32_t, k, 0u, (uint32_t)kRing) {
             uint32_t q = base + k;
             uint32_t info = 0;
             PairT p0 = 0, p1 = 0, p2 = 0, p3 = 0;
@@ -523,7 +506,7 @@ struct Enc {
         uint32_t slot = q - ring_base;
         uint32_t info = ring_info[slot];
         uint32_t cnt = info & 0xFFFFu, ml = info >> 16;
-        for (uint32_t k = lane; k < cnt; k += kWave) {
+        LANE_FOR(uint32_t, k, 0u, cnt) {
             PairT pr = k < (uint32_t)kInlinePairs ? ring_pairs[slot * kInlinePairs + k]
                                                   : ovf[ovf_off[gbase + q] + k - kInlinePairs];
             md_len[k] = (uint16_t)PP::len(pr);
@@ -572,14 +555,27 @@ struct Enc {
     // while (lenEnd < target) _optimum[++lenEnd].Price = kIfinityPrice
     FI void extend_to(uint32_t& len_end, uint32_t target) {
         if (len_end >= target) return;
-        for (uint32_t i = len_end + 1 + lane; i <= target; i += kWave) set_price(i, kInfinityPrice);
+        LANE_FOR(uint32_t, i, len_end + 1, target + 1) set_price(i, kInfinityPrice);
         len_end = target;
         fence_upto(target);
     }
     // lanes relax slots base+l, l in [lo, hi], with a rep of index ri
     FI void relax_rep(uint32_t base_slot, uint32_t lo, uint32_t hi, uint32_t price_base, uint32_t ps,
                       uint32_t pos_prev_v, uint32_t ri) {
-        for (uint32_t l = lo + lane; l <= hi; l += kWave) {
+        if (base_slot + hi < (uint32_t)kOptLds) {   // all slots in LDS: no per-lane spill branches
+            LANE_FOR(uint32_t, l, lo, hi + 1) {
+                const uint32_t cl = price_base + len_price(1, l - 2, ps), s = base_slot + l;
+                if (cl < o_price[s]) {
+                    o_price[s] = cl;
+                    o_pp[s] = (o_pp[s] & 0xFFFF0000u) | pos_prev_v;
+                    o_bp[s] = (int32_t)ri;
+                    o_fs[s] = (uint8_t)(o_fs[s] & ~1u);
+                }
+            }
+            LANE_FENCE();
+            return;
+        }
+        LANE_FOR(uint32_t, l, lo, hi + 1) {
             uint32_t cl = price_base + len_price(1, l - 2, ps);
             uint32_t s = base_slot + l;
             if (cl < price_at(s)) {
@@ -594,7 +590,20 @@ struct Enc {
     // lanes relax slots base+l, l in [lo, hi], all with the match distance `dist`
     FI void relax_match(uint32_t base_slot, uint32_t lo, uint32_t hi, uint32_t price_base, uint32_t dist, uint32_t ps,
                         uint32_t pos_prev_v) {
-        for (uint32_t l = lo + lane; l <= hi; l += kWave) {
+        if (base_slot + hi < (uint32_t)kOptLds) {   // all slots in LDS
+            LANE_FOR(uint32_t, l, lo, hi + 1) {
+                const uint32_t cl = price_base + pos_len_price(dist, l, ps), s = base_slot + l;
+                if (cl < o_price[s]) {
+                    o_price[s] = cl;
+                    o_pp[s] = (o_pp[s] & 0xFFFF0000u) | pos_prev_v;
+                    o_bp[s] = (int32_t)(dist + kNumRepDistances);
+                    o_fs[s] = (uint8_t)(o_fs[s] & ~1u);
+                }
+            }
+            LANE_FENCE();
+            return;
+        }
+        LANE_FOR(uint32_t, l, lo, hi + 1) {
             uint32_t cl = price_base + pos_len_price(dist, l, ps);
             uint32_t s = base_slot + l;
             if (cl < price_at(s)) {
@@ -725,7 +734,7 @@ struct Enc {
         set_back(0, 0, rp0); set_back(0, 1, rp1); set_back(0, 2, rp2); set_back(0, 3, rp3);
         LANE_FENCE();
         PBEGIN(t2);
-        for (uint32_t l = 2 + lane; l <= len_end; l += kWave) set_price(l, kInfinityPrice);
+        LANE_FOR(uint32_t, l, 2u, len_end + 1) set_price(l, kInfinityPrice);
         fence_upto(len_end);
 #pragma unroll
         for (uint32_t i = 0; i < (uint32_t)kNumRepDistances; i++) {
@@ -737,7 +746,7 @@ struct Enc {
         uint32_t lstart = rl0 >= 2 ? rl0 + 1 : 2;
         if (lstart <= len_main) {
             // no look-ahead in this loop: every length is independent
-            for (uint32_t l = lstart + lane; l <= len_main; l += kWave) {
+            LANE_FOR(uint32_t, l, lstart, len_main + 1) {
                 uint32_t k = 0;
                 while (k + 1 < npairs && l > md_len[k]) k++;
                 uint32_t distance = md_dist[k];
@@ -1033,9 +1042,9 @@ struct Enc {
         for (int k = 0; k < kProfSlots; k++) prof[k] = 0;
 #endif
         const uint32_t nlit = 0x300u << (lc + lp);
-        for (uint32_t i = lane; i < (uint32_t)E_COUNT; i += kWave) probs[i] = kBitModelTotal >> 1;
-        for (uint32_t i = lane; i < nlit; i += kWave) lit[i] = kBitModelTotal >> 1;
-        for (uint32_t i = lane; i < 256; i += kWave) psp[i] = 0;
+        LANE_FOR(uint32_t, i, 0u, (uint32_t)E_COUNT) probs[i] = kBitModelTotal >> 1;
+        LANE_FOR(uint32_t, i, 0u, nlit) lit[i] = kBitModelTotal >> 1;
+        LANE_FOR(uint32_t, i, 0u, 256u) psp[i] = 0;
         if (!LIT_LDS) SPILL_FENCE();
         LANE_FENCE();
         state = 0; prev_byte = 0;
@@ -1122,7 +1131,7 @@ enum { L_PP, L_PROBS, L_LENP, L_LENC, L_PSP, L_DP, L_AP, L_TP, L_MDLEN, L_MDDIST
 __host__ __device__ inline uint32_t enc_lds_layout(const EncArgs& a, uint32_t* off) {
     const uint32_t md_cap = a.fb + 2;   // pairs per position <= fb (+1 clamp slot)
     const uint32_t sz[L_COUNT] = {
-        512 * 2, enc_prob_count(a.pb) * 2, 2 * (1u << a.pb) * a.len_table_size * 2, 2 * 16 * 4, 256 * 2, 512 * 2, 16 * 4,
+        512 * 2, prob_count(a.pb) * 2, 2 * (1u << a.pb) * a.len_table_size * 2, 2 * 16 * 4, 256 * 2, 512 * 2, 16 * 4,
         kNumFullDistances * 2, md_cap * 2, md_cap * 4, kRing * 4, kRing * kInlinePairs * a.pair_bytes, kOptLds * 4, kOptLds * 4,
         kOptLds * 4, kOptLds * 4, kOptLds, 4 * kOptLds * 4, kSides * kGW, kObuf,
         a.lit_in_lds ? (0x300u << (a.lc + a.lp)) * 2 : 0u};
@@ -1165,7 +1174,7 @@ __global__ void __launch_bounds__(kWave) enc_kernel(EncArgs a) {
     uint16_t* lit_g = (uint16_t*)(scratch + kNumOpts * 4 * 9);
     if (LIT_LDS) e.lit = (uint16_t*)(smem + off[L_LIT]);
     else e.lit = lit_g;
-    for (int i = (int)e.lane; i < 512; i += kWave) e.pp[i] = (uint16_t)c_tab.prices[i];
+    for (int i0 = 0; i0 < 512; i0 += kWave) e.pp[i0 + e.lane] = (uint16_t)c_tab.prices[i0 + e.lane];
     LANE_FENCE();
     e.dbg = a.dbg;
 #ifdef LZG_DEBUG

@@ -60,6 +60,30 @@ constexpr int P_REP_LEN = P_LEN + LEN_SIZE;
 constexpr int P_LIT = P_REP_LEN + LEN_SIZE;           // literal coders follow (may live elsewhere)
 constexpr int P_FIXED_COUNT = P_LIT;                  // 1852 u16
 
+// Probability layout used by the encoder and decoder kernels (the models of
+// Encoder.java:113-128 / Decoder.java:138-152). The
+// posState-indexed models (isMatch, isRep0Long, the low/mid length coders) are
+// strided by 1 << PBS posStates: PBS = 2 serves pb <= 2 (the common case, and
+// 1.3 KiB less LDS per stream than the 16-posState layout), PBS = 4 serves pb 3-4.
+template <int PBS>
+struct ProbLayout {
+    static constexpr int IS_MATCH = 0;
+    static constexpr int IS_REP = IS_MATCH + (kNumStates << PBS);
+    static constexpr int G0 = IS_REP + kNumStates, G1 = G0 + kNumStates, G2 = G1 + kNumStates;
+    static constexpr int R0L = G2 + kNumStates;
+    static constexpr int PSLOT = R0L + (kNumStates << PBS);
+    static constexpr int PENC = PSLOT + (kNumLenToPosStates << kNumPosSlotBits);
+    static constexpr int ALIGN = PENC + (kNumFullDistances - kEndPosModelIndex);
+    static constexpr int LOW = 2, MID = LOW + (8 << PBS), HIGH = MID + (8 << PBS), LSIZE = HIGH + 256;
+    static constexpr int LEN = ALIGN + kAlignTableSize;
+    static constexpr int RLEN = LEN + LSIZE;
+    static constexpr int COUNT = RLEN + LSIZE;
+};
+__host__ __device__ inline uint32_t prob_count(uint32_t pb) {
+    return pb <= 2 ? (uint32_t)ProbLayout<2>::COUNT : (uint32_t)ProbLayout<4>::COUNT;
+}
+
+
 struct Tables {
     uint32_t crc[256];       // CRC.java:11-25 (also the BT4 hash mixer, BinTree.java:381)
     uint32_t prices[512];    // ProbPrices.java:8-18
