@@ -1,30 +1,41 @@
 // dec.hip -- batched LZMA decoder: src/main/java/SevenZip/Compression/LZMA/
-// Decoder.java (Code :205-301) with RangeDecoder.java and OutWindow.java, one
-// wavefront (kWave = 64 lanes) per independent stream, one workgroup per
-// stream (longest first).
+// Decoder.java (Code :205-301) with RangeDecoder.java, BitTreeDecoder.java and
+// OutWindow.java, one wavefront (kWave = 64 lanes) per independent stream,
+// one workgroup per stream (longest first).
 //
 // The DecodeBit chain is strictly serial, so it runs as wave-uniform scalar
-// code; the probability models live in LDS. Memory round trips are kept off
-// that chain:
+// code. What the lanes do is keep memory round trips off that chain:
+//   * bit trees are prefetched whole: before a tree is walked, every lane
+//     loads one or two of its nodes (one LDS or HBM round trip for the whole
+//     tree instead of one per bit); the walk reads the node probabilities out
+//     of the lanes (readlane) and writes each adapted probability back as it
+//     goes (the nodes along one path are distinct, so the prefetched values
+//     stay exact for the rest of the walk);
+//   * the literal coders (0x300 << (lc + lp) probabilities) live in a
+//     per-stream HBM area, so the LDS per stream stays small (fixed models,
+//     input ring, output window: ~3.5 KiB) and 16 streams share a CU; a
+//     literal's whole coder tree (plus the 8 matched-mode nodes along the
+//     match byte) is fetched in one round trip, issued before the isMatch
+//     decision so it overlaps with it;
 //   * compressed input is staged through an LDS ring (kIbuf bytes, refilled
-//     by all lanes at once), so RangeDecoder's byte reads are LDS reads;
+//     by all lanes at once);
 //   * the most recent kWin output bytes live in an LDS window (OutWindow,
-//     OutWindow.java:15-82); match copies and matched-literal bytes read it,
+//     OutWindow.java:15-82); match copies and matched-literal bytes read it
 //     with all lanes copying (an overlapping copy repeats the d-byte period:
-//     out[now + k] = out[now - d + k % d]);
-//   * the window is flushed to HBM kFlush bytes at a time (coalesced); a
-//     distance beyond half the window reads the flushed bytes in HBM.
+//     out[now + k] = out[now - d + k % d]); distances beyond half the window
+//     read the flushed bytes in HBM;
+//   * the window is flushed to HBM kFlush bytes at a time (coalesced).
 #include "lzma_common.h"
 #include "runtime.h"
 
 namespace lzg {
 
-constexpr int kDecLitLdsMaxBits = 3;
-constexpr uint32_t kIbuf = 128;     // input staging ring
+constexpr uint32_t kIbuf = 256;     // input staging ring
 constexpr uint32_t kWin = 1024;     // output window in LDS (power of two)
 constexpr uint32_t kFlush = 128;    // window -> HBM flush granule
 constexpr uint32_t kNear = kWin / 2;   // distances <= kNear read the LDS window
 static_assert(kFlush + kMatchMaxLen + 64 <= kNear, "window too small for the flush lag");
+constexpr int kVS = (64 + kWave - 1) / kWave;   // per-lane slots of a 64-entry lane vector (1 on hardware)
 
 #define DFI __device__ __forceinline__
 #define LANE_FENCE() asm volatile("" ::: "memory")
@@ -33,81 +44,88 @@ DFI uint64_t dec_uni64(uint64_t v) {
     return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32)) << 32) |
            (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
 }
+// element j (wave-uniform, < 64) of a lane vector: lane j % kWave, slot j / kWave
+DFI uint32_t vget(const uint32_t (&v)[kVS], uint32_t j) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)v[j / kWave], (int)(j % kWave));
+}
 
-// LIT_LDS: literal coders in LDS (lc + lp <= 3) or HBM. A compile-time choice,
-// so every pointer has a known address space (a generic pointer would make the
-// compiler treat each loaded model as per-lane and the whole decode as divergent).
 // PBS: posState stride of the probability layout (ProbLayout, lzma_common.h).
-template <bool LIT_LDS, int PBS>
+template <int PBS>
 struct Dec {
     using PL = ProbLayout<PBS>;
     uint32_t lane;
-    uint16_t* probs;
-    uint16_t* lit;
-    uint8_t* ibuf;                // [kIbuf]
-    uint8_t* win;                 // [kWin]
+    uint16_t* probs;              // LDS: fixed models
+    uint16_t* lit;                // HBM: literal coders of this stream
+    uint8_t* ibuf;                // LDS [kIbuf]
+    uint8_t* win;                 // LDS [kWin]
     uint32_t lc, lp, pb, ps_mask, dict_check;
     const uint8_t* in;
-    uint64_t n_in, ipos, ibase;
+    // streams < 4 GiB in and out (the host clamps the capacity): 32-bit positions keep the
+    // scalar chain free of 64-bit compares
+    uint32_t n_in, ipos, ibase, ilim;   // ilim = min(ibase + kIbuf, n_in): the fast-path bound
     uint8_t* out;
     __amdgpu_buffer_rsrc_t outb;  // the stream's output as a buffer (far reads; never merged with LDS reads)
-    uint64_t cap, flushed;
+    uint32_t cap, flushed;
     uint32_t range, code;
 
     // ---- input (InputStream.read(): -1 past the end)
-    DFI void refill(uint64_t base) {
+    DFI void refill(uint32_t base) {
         ibase = base;
+        ilim = n_in - base < kIbuf ? n_in : base + kIbuf;
         for (uint32_t k0 = 0; k0 < kIbuf; k0 += kWave) {   // uniform trip count
             const uint32_t k = k0 + lane;
-            const uint64_t q = base + k;
+            const uint32_t q = base + k;
             ibuf[k] = q < n_in ? in[q] : 0;
         }
         LANE_FENCE();
     }
     DFI uint32_t rd_byte() {
-        if (ipos >= n_in) return 0xFFFFFFFFu;
-        if (ipos - ibase >= kIbuf) refill(ipos);
-        return (uint32_t)ibuf[(uint32_t)(ipos++ - ibase)];
+        if (ipos >= ilim) {
+            if (ipos >= n_in) return 0xFFFFFFFFu;
+            refill(ipos);
+        }
+        return (uint32_t)ibuf[ipos++ - ibase];
     }
     // ---- output window
-    DFI void flush_to(uint64_t upto) {   // write [flushed, upto) to HBM (upto <= now, within the window)
+    DFI void flush_to(uint32_t upto) {   // write [flushed, upto) to HBM (upto <= now, within the window)
         LANE_FENCE();
-        for (uint64_t k0 = flushed; k0 < upto; k0 += kWave) {   // uniform trip count
-            const uint64_t k = k0 + lane;
-            if (k < upto) out[k] = win[(uint32_t)k & (kWin - 1)];
+        for (uint32_t k0 = flushed; k0 < upto; k0 += kWave) {   // uniform trip count
+            const uint32_t k = k0 + lane;
+            if (k < upto) out[k] = win[k & (kWin - 1)];
         }
         flushed = upto;
         LANE_FENCE();
     }
-    DFI void maybe_flush(uint64_t now) {
-        if (now - flushed >= kFlush) flush_to(now & ~(uint64_t)(kFlush - 1));
+    DFI void maybe_flush(uint32_t now) {
+        if (now - flushed >= kFlush) flush_to(now & ~(kFlush - 1));
     }
-    DFI uint32_t byte_back(uint64_t now, uint32_t d1) {   // out[now - d1], 1 <= d1 <= now
-        if (d1 <= kNear) return win[(uint32_t)(now - d1) & (kWin - 1)];
-        // flushed long ago (d1 > kNear > flush lag); streams < 2 GiB: 32-bit offsets
-        return __builtin_amdgcn_raw_buffer_load_b8(outb, (uint32_t)(now - d1), 0, 0);
+    DFI uint32_t byte_back(uint32_t now, uint32_t d1) {   // out[now - d1], 1 <= d1 <= now
+        if (d1 <= kNear) return win[(now - d1) & (kWin - 1)];
+        // flushed long ago (d1 > kNear > flush lag)
+        return __builtin_amdgcn_raw_buffer_load_b8(outb, now - d1, 0, 0);
     }
-    DFI void put(uint64_t now, uint32_t b) {
-        if (lane == 0) win[(uint32_t)now & (kWin - 1)] = (uint8_t)b;
+    DFI void put(uint32_t now, uint32_t b) {   // every lane stores the same byte: no exec-mask juggling
+        win[now & (kWin - 1)] = (uint8_t)b;
         LANE_FENCE();
     }
 
     // ---- range decoder
-    DFI uint32_t bit(uint16_t* p, uint32_t idx) {   // RangeDecoder.DecodeBit (RangeDecoder.java:43-64)
-        uint32_t prob = p[idx];
-        uint32_t bound = (range >> 11) * prob;
-        uint32_t r;
-        if (code < bound) {
-            range = bound;
-            p[idx] = (uint16_t)(prob + ((kBitModelTotal - prob) >> kNumMoveBits));
-            r = 0;
-        } else {
-            range -= bound;
-            code -= bound;
-            p[idx] = (uint16_t)(prob - (prob >> kNumMoveBits));
-            r = 1;
-        }
-        if ((range & kTopMask) == 0) { code = (code << 8) | rd_byte(); range <<= 8; }
+    // RangeDecoder.DecodeBit (RangeDecoder.java:43-64) on a probability already
+    // in a register; *np = the adapted probability
+    // (branch-free selects: the scalar unit is the decoder's bottleneck)
+    DFI uint32_t dbit(uint32_t prob, uint32_t* np) {
+        const uint32_t bound = (range >> 11) * prob;
+        const bool one = code >= bound;
+        range = one ? range - bound : bound;
+        code = one ? code - bound : code;
+        *np = one ? prob - (prob >> kNumMoveBits) : prob + ((kBitModelTotal - prob) >> kNumMoveBits);
+        if (range < (1u << 24)) { code = (code << 8) | rd_byte(); range <<= 8; }
+        return one ? 1u : 0u;
+    }
+    DFI uint32_t bit(uint16_t* p, uint32_t idx) {   // one decision against an LDS model
+        uint32_t np;
+        const uint32_t r = dbit(p[idx], &np);
+        p[idx] = (uint16_t)np;
         return r;
     }
     DFI uint32_t direct(int nbits) {   // RangeDecoder.DecodeDirectBits (RangeDecoder.java:27-41)
@@ -121,46 +139,113 @@ struct Dec {
         }
         return result;
     }
-    DFI uint32_t bt_dec(uint16_t* p, int nbits) {   // BitTreeDecoder.Decode (BitTreeDecoder.java:19-25)
+    // ---- prefetched trees (LDS): node m (< 64) of p in lane m
+    DFI void fetch64(const uint16_t* p, uint32_t n, uint32_t (&v)[kVS]) const {
+#pragma unroll
+        for (int s = 0; s < kVS; s++) {
+            const uint32_t m = (uint32_t)(s * kWave) + lane;
+            v[s] = m < n ? (uint32_t)p[m] : 0u;
+        }
+    }
+    // BitTreeDecoder.Decode (BitTreeDecoder.java:19-25) over a prefetched tree (nbits <= 6)
+    DFI uint32_t bt_dec(uint16_t* p, const uint32_t (&v)[kVS], int nbits) {
         uint32_t m = 1;
-        for (int b = nbits; b != 0; b--) m = (m << 1) + bit(p, m);
+        for (int b = nbits; b != 0; b--) {
+            uint32_t np;
+            const uint32_t x = dbit(vget(v, m), &np);
+            p[m] = (uint16_t)np;
+            m = (m << 1) + x;
+        }
         return m - (1u << nbits);
     }
-    DFI uint32_t bt_rev_dec(uint16_t* p, int nbits) {   // BitTreeDecoder.ReverseDecode (:27-37)
+    // BitTreeDecoder.ReverseDecode (:27-37) over a prefetched tree (nbits <= 5)
+    DFI uint32_t bt_rev_dec(uint16_t* p, const uint32_t (&v)[kVS], int nbits) {
         uint32_t m = 1, sym = 0;
-        for (int b = 0; b < nbits; b++) { uint32_t x = bit(p, m); m <<= 1; m += x; sym |= x << b; }
+        for (int b = 0; b < nbits; b++) {
+            uint32_t np;
+            const uint32_t x = dbit(vget(v, m), &np);
+            p[m] = (uint16_t)np;
+            m = (m << 1) + x;
+            sym |= x << b;
+        }
         return sym;
     }
-    DFI uint32_t len_dec(uint16_t* L, uint32_t ps) {   // Decoder.LenDecoder.Decode (Decoder.java:48-59)
-        if (bit(L, LEN_CHOICE) == 0) return bt_dec(L + PL::LOW + ps * 8, 3);
-        uint32_t sym = kNumLowLenSymbols;
-        if (bit(L, LEN_CHOICE + 1) == 0) sym += bt_dec(L + PL::MID + ps * 8, 3);
-        else sym += kNumMidLenSymbols + bt_dec(L + PL::HIGH, 8);
-        return sym;
+    // 256-node tree p[0..255] as two lane vectors of u32 pairs: nodes 2l, 2l+1 in lane l
+    // of lo (l < 64) / of hi (nodes 128 + ...). p is 4-byte aligned.
+    template <typename P>
+    DFI void fetch256(const P* p, uint32_t (&lo)[kVS], uint32_t (&hi)[kVS]) const {
+        const uint32_t* w = (const uint32_t*)p;
+#pragma unroll
+        for (int s = 0; s < kVS; s++) {
+            const uint32_t l = (uint32_t)(s * kWave) + lane;
+            lo[s] = w[l];
+            hi[s] = w[64 + l];
+        }
+    }
+    DFI static uint32_t node256(const uint32_t (&lo)[kVS], const uint32_t (&hi)[kVS], uint32_t m) {
+        const uint32_t l = (m >> 1) & 63u;
+        const uint32_t w = (m & 128u) ? vget(hi, l) : vget(lo, l);
+        return (w >> ((m & 1u) << 4)) & 0xFFFFu;
+    }
+    // Decoder.LenDecoder.Decode (Decoder.java:48-59) over prefetched nodes:
+    // lv lanes 0-7 low[ps], 8-15 mid[ps], 16-17 the two choices; lo/hi the high tree
+    DFI void fetch_len(const uint16_t* L, uint32_t ps, uint32_t (&lv)[kVS], uint32_t (&lo)[kVS], uint32_t (&hi)[kVS]) const {
+#pragma unroll
+        for (int s = 0; s < kVS; s++) {
+            const uint32_t m = (uint32_t)(s * kWave) + lane;
+            uint32_t v = 0;
+            if (m < 8) v = L[PL::LOW + ps * 8 + m];
+            else if (m < 16) v = L[PL::MID + ps * 8 + m - 8];
+            else if (m < 18) v = L[LEN_CHOICE + m - 16];
+            lv[s] = v;
+        }
+        fetch256(L + PL::HIGH, lo, hi);
+    }
+    DFI uint32_t len_dec(uint16_t* L, uint32_t ps, const uint32_t (&lv)[kVS], const uint32_t (&lo)[kVS],
+                         const uint32_t (&hi)[kVS]) {
+        uint32_t np;
+        uint32_t x = dbit(vget(lv, 16), &np);
+        L[LEN_CHOICE] = (uint16_t)np;
+        uint32_t base, off, nb, sym0;
+        if (x == 0) { base = PL::LOW + ps * 8; off = 0; nb = 3; sym0 = 0; }
+        else {
+            x = dbit(vget(lv, 17), &np);
+            L[LEN_CHOICE + 1] = (uint16_t)np;
+            if (x == 0) { base = PL::MID + ps * 8; off = 8; nb = 3; sym0 = kNumLowLenSymbols; }
+            else { base = PL::HIGH; off = 0; nb = 8; sym0 = kNumLowLenSymbols + kNumMidLenSymbols; }
+        }
+        uint32_t m = 1;
+        for (uint32_t b = nb; b != 0; b--) {
+            const uint32_t prob = nb == 3 ? vget(lv, off + m) : node256(lo, hi, m);
+            x = dbit(prob, &np);
+            L[base + m] = (uint16_t)np;
+            m = (m << 1) + x;
+        }
+        return sym0 + m - (1u << nb);
     }
     // OutWindow.CopyBlock (OutWindow.java:53-67) of len bytes at distance d1,
     // byte-serial semantics: an overlapping copy repeats the d1-byte period.
-    DFI void copy(uint64_t now, uint32_t d1, uint32_t len) {
+    DFI void copy(uint32_t now, uint32_t d1, uint32_t len) {
         LANE_FENCE();
         for (uint32_t k0 = 0; k0 < len; k0 += kWave) {
             const uint32_t k = k0 + lane;
             if (k < len) {
                 // source = now - d1 + (k mod d1): always before `now`, so lanes never
                 // read a byte this copy writes (and kNear + 273 < kWin: no ring alias)
-                const uint32_t r = k % d1;
-                win[(uint32_t)(now + k) & (kWin - 1)] = (uint8_t)byte_back(now, d1 - r);
+                const uint32_t r = d1 > len ? k : k % d1;
+                win[(now + k) & (kWin - 1)] = (uint8_t)byte_back(now, d1 - r);
             }
         }
         LANE_FENCE();
     }
 
     // returns LZMA_OK / LZMA_E_DATA / LZMA_E_OVERFLOW; *now_out = bytes written
-    DFI int run(int64_t out_size, uint64_t* now_out) {
+    DFI int run(int64_t out_size, uint32_t* now_out) {
         const uint32_t nlit = 0x300u << (lc + lp);
         for (uint32_t i0 = 0; i0 < (uint32_t)PL::COUNT; i0 += kWave)
             if (i0 + lane < (uint32_t)PL::COUNT) probs[i0 + lane] = kBitModelTotal >> 1;
-        for (uint32_t i0 = 0; i0 < nlit; i0 += kWave)
-            if (i0 + lane < nlit) lit[i0 + lane] = kBitModelTotal >> 1;
+        for (uint32_t i0 = 0; i0 < nlit; i0 += 2 * kWave)   // u32 pairs (nlit is even)
+            if (i0 + 2 * lane < nlit) *(uint32_t*)(lit + i0 + 2 * lane) = (kBitModelTotal >> 1) * 0x10001u;
         LANE_FENCE();
         ipos = 0;
         ibase = 0;
@@ -170,28 +255,44 @@ struct Dec {
         range = 0xFFFFFFFFu;
         for (int i = 0; i < 5; i++) code = (code << 8) | rd_byte();   // RangeDecoder.Init
         uint32_t state = 0, rep0 = 0, rep1 = 0, rep2 = 0, rep3 = 0;
-        uint64_t now = 0;
+        uint32_t now = 0;
         uint32_t prev = 0;
         int rc = LZMA_OK;
-        while (out_size < 0 || (int64_t)now < out_size) {
-            const uint32_t ps = (uint32_t)now & ps_mask;
+        // out_size >= 0: stop after out_size bytes (capped at 2^32 - 1, beyond any capacity)
+        const uint32_t stop = out_size < 0 || out_size > 0xFFFFFFFFll ? 0xFFFFFFFFu : (uint32_t)out_size;
+        while (out_size < 0 || now < stop) {
+            const uint32_t ps = now & ps_mask;
+            // literal prefetch, issued before the isMatch decision: the coder's tree
+            // (nodes 0-255) and, in matched mode, the 8 nodes along the match byte
+            const bool matched = !st_is_char(state);
+            const uint32_t mb = matched ? byte_back(now, rep0 + 1) : 0u;
+            uint16_t* sub = lit + (size_t)(((now & ((1u << lp) - 1)) << lc) + (prev >> (8 - lc))) * 0x300;
+            uint32_t tlo[kVS], thi[kVS], mv[kVS];
+            fetch256(sub, tlo, thi);
+#pragma unroll
+            for (int s = 0; s < kVS; s++) {
+                const uint32_t i = (uint32_t)(s * kWave) + lane;
+                mv[s] = 0;
+                if (matched && i < 8) {   // level i: prefix of mb with the leading 1, match bit 7 - i
+                    const uint32_t mbit = (mb >> (7 - i)) & 1u;
+                    mv[s] = sub[((1 + mbit) << 8) + ((0x100u | mb) >> (8 - i))];
+                }
+            }
+            LANE_FENCE();   // keeps the loads here (not sunk into the literal branch)
             if (bit(probs + PL::IS_MATCH, (state << PBS) + ps) == 0) {
-                uint16_t* sub = lit + (size_t)((((uint32_t)now & ((1u << lp) - 1)) << lc) + (prev >> (8 - lc))) * 0x300;
+                // LiteralDecoder.Decoder2.DecodeNormal / DecodeWithMatchByte (Decoder.java:67-102)
                 uint32_t sym = 1;
-                if (st_is_char(state)) {
-                    do { sym = (sym << 1) | bit(sub, sym); } while (sym < 0x100);
-                } else {   // LiteralDecoder.Decoder2.DecodeWithMatchByte (Decoder.java:80-102)
-                    uint32_t mb = byte_back(now, rep0 + 1);
-                    do {
-                        uint32_t mbit = (mb >> 7) & 1;
-                        mb <<= 1;
-                        uint32_t b = bit(sub, ((1 + mbit) << 8) + sym);
-                        sym = (sym << 1) | b;
-                        if (mbit != b) {
-                            while (sym < 0x100) sym = (sym << 1) | bit(sub, sym);
-                            break;
-                        }
-                    } while (sym < 0x100);
+                bool same = matched;
+#pragma unroll 1
+                for (uint32_t i = 0; i < 8; i++) {
+                    uint32_t np, idx, prob;
+                    const uint32_t mbit = (mb >> (7 - i)) & 1u;
+                    if (same) { idx = ((1 + mbit) << 8) + sym; prob = vget(mv, i); }
+                    else { idx = sym; prob = node256(tlo, thi, sym); }
+                    const uint32_t x = dbit(prob, &np);
+                    sub[idx] = (uint16_t)np;   // every lane, same address and value
+                    if (same && x != mbit) same = false;
+                    sym = (sym << 1) | x;
                 }
                 prev = sym & 0xFF;
                 if (now >= cap) { rc = LZMA_E_OVERFLOW; break; }
@@ -200,7 +301,9 @@ struct Dec {
                 state = st_lit(state);
             } else {
                 uint32_t len;
+                uint32_t lv[kVS], lo[kVS], hi[kVS];
                 if (bit(probs + PL::IS_REP, state) == 1) {
+                    fetch_len(probs + PL::RLEN, ps, lv, lo, hi);
                     len = 0;
                     if (bit(probs + PL::G0, state) == 0) {
                         if (bit(probs + PL::R0L, (state << PBS) + ps) == 0) { state = st_short(state); len = 1; }
@@ -215,20 +318,28 @@ struct Dec {
                         rep1 = rep0;
                         rep0 = dist;
                     }
-                    if (len == 0) { len = len_dec(probs + PL::RLEN, ps) + kMatchMinLen; state = st_long(state); }
+                    if (len == 0) { len = len_dec(probs + PL::RLEN, ps, lv, lo, hi) + kMatchMinLen; state = st_long(state); }
                 } else {
+                    fetch_len(probs + PL::LEN, ps, lv, lo, hi);
                     rep3 = rep2; rep2 = rep1; rep1 = rep0;
-                    len = kMatchMinLen + len_dec(probs + PL::LEN, ps);
+                    len = kMatchMinLen + len_dec(probs + PL::LEN, ps, lv, lo, hi);
                     state = st_match(state);
-                    uint32_t slot = bt_dec(probs + PL::PSLOT + (len_to_pos_state(len) << 6), kNumPosSlotBits);
+                    uint16_t* slot_p = probs + PL::PSLOT + (len_to_pos_state(len) << 6);
+                    uint32_t sv[kVS], av[kVS];
+                    fetch64(slot_p, 64, sv);
+                    fetch64(probs + PL::ALIGN, kAlignTableSize, av);
+                    const uint32_t slot = bt_dec(slot_p, sv, kNumPosSlotBits);
                     if (slot >= (uint32_t)kStartPosModelIndex) {
                         uint32_t ndb = (slot >> 1) - 1;
                         rep0 = (2 | (slot & 1)) << ndb;
                         if (slot < (uint32_t)kEndPosModelIndex) {
-                            rep0 += bt_rev_dec(probs + PL::PENC + (int32_t)(rep0 - slot - 1), (int)ndb);
+                            uint16_t* pe = probs + PL::PENC + (int32_t)(rep0 - slot - 1);
+                            uint32_t pv[kVS];
+                            fetch64(pe, 1u << ndb, pv);
+                            rep0 += bt_rev_dec(pe, pv, (int)ndb);
                         } else {
                             rep0 += direct((int)(ndb - kNumAlignBits)) << kNumAlignBits;
-                            rep0 += bt_rev_dec(probs + PL::ALIGN, kNumAlignBits);
+                            rep0 += bt_rev_dec(probs + PL::ALIGN, av, kNumAlignBits);
                             if ((int32_t)rep0 < 0) {
                                 if (rep0 == 0xFFFFFFFFu) break;   // end marker
                                 rc = LZMA_E_DATA;
@@ -239,10 +350,10 @@ struct Dec {
                         rep0 = slot;
                     }
                 }
-                if ((uint64_t)rep0 >= now || rep0 >= dict_check) { rc = LZMA_E_DATA; break; }
+                if (rep0 >= now || rep0 >= dict_check) { rc = LZMA_E_DATA; break; }
                 const uint32_t d1 = rep0 + 1;
-                if (now + len > cap) {   // copy what fits, then report (no bytes past the capacity)
-                    const uint32_t fit = (uint32_t)(cap - now);
+                if ((uint64_t)now + len > cap) {   // copy what fits, then report (no bytes past the capacity)
+                    const uint32_t fit = cap - now;
                     copy(now, d1, fit);
                     now = cap;
                     rc = LZMA_E_OVERFLOW;
@@ -250,7 +361,7 @@ struct Dec {
                 }
                 copy(now, d1, len);
                 now += len;
-                prev = win[(uint32_t)(now - 1) & (kWin - 1)];
+                prev = win[(now - 1) & (kWin - 1)];
             }
             maybe_flush(now);
         }
@@ -260,10 +371,10 @@ struct Dec {
     }
 };
 
-template <bool LIT_LDS, int PBS>
+template <int PBS>
 __global__ void __launch_bounds__(kWave) dec_kernel(DecArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    Dec<LIT_LDS, PBS> d;
+    Dec<PBS> d;
     d.lane = threadIdx.x;
     d.lc = a.lc; d.lp = a.lp; d.pb = a.pb; d.ps_mask = (1u << a.pb) - 1; d.dict_check = a.dict_check;
     size_t off = 0;
@@ -271,47 +382,42 @@ __global__ void __launch_bounds__(kWave) dec_kernel(DecArgs a) {
     d.probs = (uint16_t*)take((size_t)ProbLayout<PBS>::COUNT * 2);
     d.ibuf = take(kIbuf);
     d.win = take(kWin);
-    if (LIT_LDS) d.lit = (uint16_t*)take(((size_t)0x300 << (a.lc + a.lp)) * 2);
-    else d.lit = (uint16_t*)(a.scratch + (size_t)blockIdx.x * a.scratch_stride);
+    d.lit = (uint16_t*)(a.scratch + (size_t)blockIdx.x * a.scratch_stride);
     // one workgroup per stream; per-stream values are wave-uniform (readfirstlane keeps them scalar)
     const int s = __builtin_amdgcn_readfirstlane((int)a.order[blockIdx.x]);
     const uint64_t i0 = dec_uni64(a.in_offs[s]), o0 = dec_uni64(a.out_offs[s]);
     d.in = a.in + i0;
-    d.n_in = dec_uni64(a.in_offs[s + 1]) - i0;
+    const uint64_t n_in = dec_uni64(a.in_offs[s + 1]) - i0, cap = dec_uni64(a.out_offs[s + 1]) - o0;
+    d.n_in = n_in > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)n_in;   // the host rejects inputs >= 4 GiB
     d.out = a.out + o0;
-    d.cap = dec_uni64(a.out_offs[s + 1]) - o0;
-    d.outb = __builtin_amdgcn_make_buffer_rsrc(d.out, 0, d.cap > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)d.cap, 0x00020000);
+    d.cap = cap > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)cap;
+    d.outb = __builtin_amdgcn_make_buffer_rsrc(d.out, 0, d.cap, 0x00020000);
     const int64_t out_size = (int64_t)dec_uni64((uint64_t)a.out_sizes[s]);
-    uint64_t now = 0;
+    uint32_t now = 0;
     int rc = d.run(out_size, &now);
     if (d.lane == 0) { a.out_lens[s] = now; a.status[s] = rc; }
 }
 
+// literal coders of one stream (HBM), 256-byte aligned
 size_t dec_scratch_per_block(uint32_t lc, uint32_t lp) { return ((size_t)0x300 << (lc + lp)) * 2 + 256; }
 
-static size_t dec_lds_bytes(uint32_t lc, uint32_t lp, uint32_t pb, uint32_t lit_in_lds) {
+static size_t dec_lds_bytes(uint32_t pb) {
     auto r = [](size_t b) { return (b + 15) & ~(size_t)15; };
-    size_t lds = r((size_t)prob_count(pb) * 2) + r(kIbuf) + r(kWin);
-    if (lit_in_lds) lds += r(((size_t)0x300 << (lc + lp)) * 2);
-    return lds;
+    return r((size_t)prob_count(pb) * 2) + r(kIbuf) + r(kWin);
 }
 
 int dec_grid(uint32_t, uint32_t, uint32_t, int nstreams) { return nstreams; }   // one workgroup per stream
 
-template <bool LIT, int PBS>
+template <int PBS>
 static void launch_dec(const DecArgs& a, int grid, size_t lds, hipStream_t st) {
-    if (lds > 64 * 1024) hipFuncSetAttribute((const void*)dec_kernel<LIT, PBS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL((dec_kernel<LIT, PBS>), dim3(grid), dim3(kWave), lds, st, a);
+    hipLaunchKernelGGL((dec_kernel<PBS>), dim3(grid), dim3(kWave), lds, st, a);
 }
 
 int launch_decoder(Ctx* ctx, const DecArgs& a, int grid, hipStream_t st) {
-    size_t lds = dec_lds_bytes(a.lc, a.lp, a.pb, a.lit_in_lds);
+    if (a.lit_in_lds || a.scratch == nullptr) return ctx->fail(LZMA_E_INTERNAL, "decoder needs the literal-coder scratch");
+    const size_t lds = dec_lds_bytes(a.pb);
     TimedLaunch tl(ctx, "dec_stream", st);
-    if (a.lit_in_lds) {
-        if (a.pb <= 2) launch_dec<true, 2>(a, grid, lds, st); else launch_dec<true, 4>(a, grid, lds, st);
-    } else {
-        if (a.pb <= 2) launch_dec<false, 2>(a, grid, lds, st); else launch_dec<false, 4>(a, grid, lds, st);
-    }
+    if (a.pb <= 2) launch_dec<2>(a, grid, lds, st); else launch_dec<4>(a, grid, lds, st);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return ctx->fail(LZMA_E_DEVICE, "dec launch: %s", hipGetErrorString(e));
     return LZMA_OK;

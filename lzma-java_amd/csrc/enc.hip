@@ -29,6 +29,8 @@
 #include "lzma_common.h"
 #include "runtime.h"
 
+#include <type_traits>
+
 namespace lzg {
 
 static __constant__ Tables c_tab = make_tables();
@@ -87,6 +89,16 @@ FI uint64_t uni64(uint64_t v) {
 template <int N>
 FI uint32_t lane_value(const uint32_t (&v)[N], int j) {
     return (uint32_t)__builtin_amdgcn_readlane((int)v[j / kWave], j % kWave);
+}
+
+FI uint32_t brev32(uint32_t v) {
+#if defined(__clang__)
+    return __builtin_bitreverse32(v);
+#else
+    uint32_t r = 0;
+    for (int i = 0; i < 32; i++) r |= ((v >> i) & 1u) << (31 - i);
+    return r;
+#endif
 }
 
 FI uint32_t sel4(uint32_t i, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
@@ -357,68 +369,133 @@ struct Enc {
         cache_size++;
         low = (low & 0xFFFFFFull) << 8;
     }
-    FI void rc_bit(uint16_t* p, uint32_t idx, uint32_t bit) {
-        uint32_t prob = p[idx];
-        uint32_t bound = (range >> 11) * prob;
-        if (bit == 0) { range = bound; p[idx] = (uint16_t)(prob + ((kBitModelTotal - prob) >> kNumMoveBits)); }
-        else { low += bound; range -= bound; p[idx] = (uint16_t)(prob - (prob >> kNumMoveBits)); }
-        if ((range & kTopMask) == 0) { range <<= 8; shift_low(); }
+    // ------------------------------------------------------------ symbol coder
+    // One coded symbol (literal, rep, match or the end marker) is the sequence
+    // of binary decisions Encoder.java:890-1024 / :818-835 make. Within one
+    // symbol every decision uses a distinct probability (bit-tree nodes along
+    // one path are distinct, each model is visited at most once), so the
+    // decisions are laid out one per lane (q_* below), every lane loads its
+    // probability at once, the range coder (RangeEncoder.Encode/
+    // EncodeDirectBits, RangeEncoder.java:38-77) runs serially over the
+    // register copies, and the lanes write the adapted probabilities back at
+    // once. The coder loop is the only range-coder instance in the kernel.
+    static constexpr int kQS = (64 + kWave - 1) / kWave;   // decision slots per lane (1 on hardware)
+    enum : uint32_t { QK_NONE = 0, QK_PROB = 1, QK_LIT = 2, QK_DIRECT = 3 };
+    struct Q {
+        uint32_t n;
+        uint32_t idx[kQS], bit[kQS], kind[kQS];
+    };
+    FI void q_init(Q& q) const {
+        q.n = 0;
+#pragma unroll
+        for (int t = 0; t < kQS; t++) { q.idx[t] = 0; q.bit[t] = 0; q.kind[t] = QK_NONE; }
     }
-    FI void rc_direct(uint32_t v, int nbits) {
-        for (int i = nbits - 1; i >= 0; i--) {
-            range >>= 1;
-            if ((v >> i) & 1) low += range;
-            if ((range & kTopMask) == 0) { range <<= 8; shift_low(); }
+    // one decision against probs[index]
+    FI void q_bit(Q& q, uint32_t index, uint32_t bit) const {
+#pragma unroll
+        for (int t = 0; t < kQS; t++)
+            if ((uint32_t)(t * kWave) + lane == q.n) { q.idx[t] = index; q.bit[t] = bit; q.kind[t] = QK_PROB; }
+        q.n++;
+    }
+    // BitTreeEncoder.Encode (BitTreeEncoder.java:18-27): node of bit i (MSB first) = the i-bit prefix
+    FI void q_bt(Q& q, uint32_t base, uint32_t nbits, uint32_t sym) const {
+#pragma unroll
+        for (int t = 0; t < kQS; t++) {
+            const uint32_t i = (uint32_t)(t * kWave) + lane - q.n;
+            if (i < nbits) {
+                q.idx[t] = base + ((sym | (1u << nbits)) >> (nbits - i));
+                q.bit[t] = (sym >> (nbits - 1 - i)) & 1u;
+                q.kind[t] = QK_PROB;
+            }
         }
+        q.n += nbits;
     }
-    FI void bt_enc(uint16_t* p, int nbits, uint32_t sym) {
-        uint32_t m = 1;
-        for (int b = nbits; b != 0;) { b--; uint32_t bit = (sym >> b) & 1; rc_bit(p, m, bit); m = (m << 1) | bit; }
+    // BitTreeEncoder.ReverseEncode (BitTreeEncoder.java:29-36, Encoder.java:196-205): bit i (LSB first)
+    // at node 1 followed by bits 0..i-1
+    FI void q_rev(Q& q, uint32_t base, uint32_t nbits, uint32_t sym) const {
+#pragma unroll
+        for (int t = 0; t < kQS; t++) {
+            const uint32_t i = (uint32_t)(t * kWave) + lane - q.n;
+            if (i < nbits) {
+                const uint32_t m = (1u << i) | (i ? brev32(sym) >> (32 - i) : 0u);
+                q.idx[t] = base + m;
+                q.bit[t] = (sym >> i) & 1u;
+                q.kind[t] = QK_PROB;
+            }
+        }
+        q.n += nbits;
     }
-    FI void bt_rev_enc(uint16_t* p, int nbits, uint32_t sym) {
-        uint32_t m = 1;
-        for (int i = 0; i < nbits; i++) { uint32_t bit = sym & 1; rc_bit(p, m, bit); m = (m << 1) | bit; sym >>= 1; }
+    // RangeEncoder.EncodeDirectBits (RangeEncoder.java:41-51), MSB first
+    FI void q_direct(Q& q, uint32_t v, uint32_t nbits) const {
+#pragma unroll
+        for (int t = 0; t < kQS; t++) {
+            const uint32_t i = (uint32_t)(t * kWave) + lane - q.n;
+            if (i < nbits) { q.bit[t] = (v >> (nbits - 1 - i)) & 1u; q.kind[t] = QK_DIRECT; }
+        }
+        q.n += nbits;
     }
-    // LiteralEncoder.Encoder2.encode / encodeMatched (LiteralEncoder.java:17-40).
-    // The 8 model indices depend only on (sym, mb), and they are distinct, so
-    // the probabilities are read in one step (lane j <-> bit 7-j), the range
-    // coder runs on the register copies, and lanes write the updated models
-    // back in one step: one memory round trip per literal even when the
-    // coders live in HBM.
-    FI void lit_encode(uint16_t* p, bool matched, uint32_t mb, uint32_t sym) {
+    // LiteralEncoder.Encoder2.Encode / EncodeMatched (LiteralEncoder.java:17-40) against the
+    // coder at lit[base]: matched context while every higher bit equals the match byte's
+    FI void q_lit(Q& q, uint32_t base, bool matched, uint32_t mb, uint32_t sym) const {
         int first = -1;
         if (matched) {
             const uint32_t diff = (mb ^ sym) & 0xFFu;
             first = diff ? 31 - __clz(diff) : -1;
         }
-        uint32_t pr[kLitSlots], ix[kLitSlots];
 #pragma unroll
-        for (int t = 0; t < kLitSlots; t++) {
-            const int j = t * kWave + (int)lane;
-            ix[t] = 0; pr[t] = 0;
-            if (j < 8) {
-                const int i = 7 - j;
+        for (int t = 0; t < kQS; t++) {
+            const uint32_t j = (uint32_t)(t * kWave) + lane - q.n;
+            if (j < 8u) {
+                const int i = 7 - (int)j;
                 const uint32_t ctx = (0x100u | sym) >> (i + 1);
-                ix[t] = (matched && i >= first) ? ((1 + ((mb >> i) & 1)) << 8) + ctx : ctx;
-                pr[t] = p[ix[t]];
+                q.idx[t] = base + ((matched && i >= first) ? ((1 + ((mb >> i) & 1)) << 8) + ctx : ctx);
+                q.bit[t] = (sym >> i) & 1u;
+                q.kind[t] = QK_LIT;
             }
         }
+        q.n += 8;
+    }
+    // LenEncoder.Encode (LenEncoder.java:24-39)
+    FI void q_len(Q& q, int which, uint32_t sym, uint32_t ps) const {
+        const uint32_t L = which ? E_RLEN : E_LEN;
+        if (sym < (uint32_t)kNumLowLenSymbols) { q_bit(q, L + LEN_CHOICE, 0); q_bt(q, L + E_LOW + ps * 8, 3, sym); }
+        else {
+            sym -= kNumLowLenSymbols;
+            q_bit(q, L + LEN_CHOICE, 1);
+            if (sym < (uint32_t)kNumMidLenSymbols) { q_bit(q, L + LEN_CHOICE + 1, 0); q_bt(q, L + E_MID + ps * 8, 3, sym); }
+            else { q_bit(q, L + LEN_CHOICE + 1, 1); q_bt(q, L + E_HIGH, 8, sym - kNumMidLenSymbols); }
+        }
+    }
+    FI void q_run(const Q& q) {
+        uint32_t pr[kQS];
+        uint64_t bm = 0, dm = 0;
 #pragma unroll
-        for (int j = 0; j < 8; j++) {
-            const uint32_t prob = lane_value(pr, j);
-            const uint32_t bound = (range >> 11) * prob;
-            if ((sym >> (7 - j)) & 1) { low += bound; range -= bound; }
-            else range = bound;
+        for (int t = 0; t < kQS; t++) {
+            pr[t] = 0;
+            if (q.kind[t] == QK_LIT) pr[t] = lit[q.idx[t]];
+            else if (q.kind[t] == QK_PROB) pr[t] = probs[q.idx[t]];
+            bm |= (uint64_t)__ballot(q.bit[t] != 0) << (t * kWave);
+            dm |= (uint64_t)__ballot(q.kind[t] == QK_DIRECT) << (t * kWave);
+        }
+#pragma unroll 1
+        for (uint32_t j = 0; j < q.n; j++) {
+            const uint32_t b = (uint32_t)(bm >> j) & 1u;
+            if ((dm >> j) & 1u) {
+                range >>= 1;
+                if (b) low += range;
+            } else {
+                const uint32_t bound = (range >> 11) * lane_value(pr, (int)j);
+                if (b) { low += bound; range -= bound; }
+                else range = bound;
+            }
             if ((range & kTopMask) == 0) { range <<= 8; shift_low(); }
         }
 #pragma unroll
-        for (int t = 0; t < kLitSlots; t++) {
-            const int j = t * kWave + (int)lane;
-            if (j < 8) {
-                const uint32_t q = pr[t];
-                p[ix[t]] = (uint16_t)(((sym >> (7 - j)) & 1) ? q - (q >> kNumMoveBits)
-                                                            : q + ((kBitModelTotal - q) >> kNumMoveBits));
-            }
+        for (int t = 0; t < kQS; t++) {
+            const uint32_t p = pr[t];
+            const uint16_t np = (uint16_t)(q.bit[t] ? p - (p >> kNumMoveBits) : p + ((kBitModelTotal - p) >> kNumMoveBits));
+            if (q.kind[t] == QK_LIT) lit[q.idx[t]] = np;
+            else if (q.kind[t] == QK_PROB) probs[q.idx[t]] = np;
         }
         LANE_FENCE();
     }
@@ -438,19 +515,6 @@ struct Enc {
         }
         lenc[which * 16 + ps] = tsize;
         LANE_FENCE();
-    }
-    FI void len_encode(int which, uint32_t sym, uint32_t ps) {   // LenEncoder.java:24-39 + LenPriceTableEncoder.java:31-37
-        uint16_t* L = probs + (which ? E_RLEN : E_LEN);
-        if (sym < (uint32_t)kNumLowLenSymbols) { rc_bit(L, LEN_CHOICE, 0); bt_enc(L + E_LOW + ps * 8, 3, sym); }
-        else {
-            sym -= kNumLowLenSymbols;
-            rc_bit(L, LEN_CHOICE, 1);
-            if (sym < (uint32_t)kNumMidLenSymbols) { rc_bit(L, LEN_CHOICE + 1, 0); bt_enc(L + E_MID + ps * 8, 3, sym); }
-            else { rc_bit(L, LEN_CHOICE + 1, 1); bt_enc(L + E_HIGH, 8, sym - kNumMidLenSymbols); }
-        }
-        uint32_t c = lenc[which * 16 + ps] - 1;
-        lenc[which * 16 + ps] = c;
-        if (c == 0) update_len_table(which, ps);
     }
     FI void fill_distances_prices() {   // Encoder.java:1087-1118
         LANE_FOR(uint32_t, i, (uint32_t)kStartPosModelIndex, (uint32_t)kNumFullDistances) {
@@ -979,60 +1043,75 @@ struct Enc {
         }
     }
 
-    // ------------------------------------------------------------ emitters (Encoder.java:938-1024, 818-841)
-    FI void encode_rep(int32_t pos, uint32_t len, uint32_t ps, uint32_t cs) {
-        rc_bit(probs + E_IS_REP, state, 1);
-        if (pos == 0) {
-            rc_bit(probs + E_G0, state, 0);
-            rc_bit(probs + E_R0L, cs, len == 1 ? 0 : 1);
+    // ------------------------------------------------------------ emitters (Encoder.java:860-1024, 818-841)
+    // Codes one symbol: back = -1 literal (cb, match byte mb), 0..3 rep, >= 4 match
+    // (distance back - 4); eos_marker codes WriteEndMarker's pseudo-match instead.
+    FI void encode_symbol(int32_t back, uint32_t len, uint32_t now_pos, uint32_t cb, uint32_t mb, bool eos_marker) {
+        Q q;
+        q_init(q);
+        const uint32_t ps = now_pos & ps_mask;
+        int len_coder = -1;
+        if (back == -1 && !eos_marker) {   // encodeSingleByteLiteral path (Encoder.java:893-903)
+            q_bit(q, E_IS_MATCH + (state << PBS) + ps, 0);
+            const uint32_t cidx = ((now_pos & ((1u << lp) - 1)) << lc) + (prev_byte >> (8 - lc));
+            q_lit(q, cidx * 0x300u, !st_is_char(state), mb, cb);
+            state = st_lit(state);
+            prev_byte = cb;
         } else {
-            rc_bit(probs + E_G0, state, 1);
-            if (pos == 1) rc_bit(probs + E_G1, state, 0);
-            else { rc_bit(probs + E_G1, state, 1); rc_bit(probs + E_G2, state, (uint32_t)pos - 2); }
-        }
-        if (len == 1) state = st_short(state);
-        else { len_encode(1, len - kMatchMinLen, ps); state = st_long(state); }
-        if (pos == 1) { uint32_t t = rd1; rd1 = rd0; rd0 = t; }
-        else if (pos == 2) { uint32_t t = rd2; rd2 = rd1; rd1 = rd0; rd0 = t; }
-        else if (pos == 3) { uint32_t t = rd3; rd3 = rd2; rd2 = rd1; rd1 = rd0; rd0 = t; }
-    }
-    FI void encode_match(int32_t backp, uint32_t len, uint32_t ps) {
-        rc_bit(probs + E_IS_REP, state, 0);
-        state = st_match(state);
-        len_encode(0, len - kMatchMinLen, ps);
-        uint32_t pos = (uint32_t)(backp - kNumRepDistances);
-        uint32_t slot;
-        if (pos < (1u << 11)) slot = c_tab.fastpos[pos];
-        else if (pos < (1u << 21)) slot = c_tab.fastpos[pos >> 10] + 20;
-        else slot = c_tab.fastpos[pos >> 20] + 40;
-        bt_enc(probs + E_PSLOT + (len_to_pos_state(len) << 6), kNumPosSlotBits, slot);
-        if (slot >= (uint32_t)kStartPosModelIndex) {
-            uint32_t footer = (slot >> 1) - 1, base = (2 | (slot & 1)) << footer, red = pos - base;
-            if (slot < (uint32_t)kEndPosModelIndex) {
-                uint16_t* m = probs + E_PENC + (int32_t)(base - slot - 1);
-                uint32_t mm = 1, sym = red;
-                for (uint32_t i = 0; i < footer; i++) { uint32_t bit = sym & 1; rc_bit(m, mm, bit); mm = (mm << 1) | bit; sym >>= 1; }
-            } else {
-                rc_direct(red >> kNumAlignBits, (int)(footer - kNumAlignBits));
-                bt_rev_enc(probs + E_ALIGN, kNumAlignBits, red & kAlignMask);
-                align_price_count++;
+            q_bit(q, E_IS_MATCH + (state << PBS) + ps, 1);
+            if (back >= 0 && back < kNumRepDistances && !eos_marker) {   // encodeARepetition (Encoder.java:938-974)
+                q_bit(q, E_IS_REP + state, 1);
+                if (back == 0) {
+                    q_bit(q, E_G0 + state, 0);
+                    q_bit(q, E_R0L + (state << PBS) + ps, len == 1 ? 0 : 1);
+                } else {
+                    q_bit(q, E_G0 + state, 1);
+                    if (back == 1) q_bit(q, E_G1 + state, 0);
+                    else { q_bit(q, E_G1 + state, 1); q_bit(q, E_G2 + state, (uint32_t)back - 2); }
+                }
+                if (len == 1) state = st_short(state);
+                else { q_len(q, 1, len - kMatchMinLen, ps); len_coder = 1; state = st_long(state); }
+                if (back == 1) { uint32_t t = rd1; rd1 = rd0; rd0 = t; }
+                else if (back == 2) { uint32_t t = rd2; rd2 = rd1; rd1 = rd0; rd0 = t; }
+                else if (back == 3) { uint32_t t = rd3; rd3 = rd2; rd2 = rd1; rd1 = rd0; rd0 = t; }
+            } else {   // encodeAMatch (Encoder.java:976-1005); the end marker is the match
+                       // (len 2, slot 63, reduced distance 2^30 - 1) of WriteEndMarker (:818-835)
+                q_bit(q, E_IS_REP + state, 0);
+                state = st_match(state);
+                q_len(q, 0, len - kMatchMinLen, ps);
+                len_coder = 0;
+                const uint32_t pos = eos_marker ? 0xFFFFFFFFu : (uint32_t)(back - kNumRepDistances);
+                uint32_t slot;
+                if (eos_marker) slot = 63;
+                else if (pos < (1u << 11)) slot = c_tab.fastpos[pos];
+                else if (pos < (1u << 21)) slot = c_tab.fastpos[pos >> 10] + 20;
+                else slot = c_tab.fastpos[pos >> 20] + 40;
+                q_bt(q, E_PSLOT + (len_to_pos_state(len) << 6), kNumPosSlotBits, slot);
+                if (slot >= (uint32_t)kStartPosModelIndex) {
+                    const uint32_t footer = (slot >> 1) - 1, base = (2 | (slot & 1)) << footer, red = pos - base;
+                    if (slot < (uint32_t)kEndPosModelIndex) q_rev(q, E_PENC + base - slot - 1, footer, red);
+                    else {
+                        q_direct(q, red >> kNumAlignBits, footer - kNumAlignBits);
+                        q_rev(q, E_ALIGN, kNumAlignBits, red & kAlignMask);
+                        align_price_count++;
+                    }
+                }
+                rd3 = rd2; rd2 = rd1; rd1 = rd0; rd0 = pos;
+                match_price_count++;
             }
+            prev_byte = cb;   // the match's last byte
         }
-        rd3 = rd2; rd2 = rd1; rd1 = rd0; rd0 = pos;
-        match_price_count++;
+        q_run(q);
+        if (len_coder >= 0) {   // LenPriceTableEncoder.Encode (LenPriceTableEncoder.java:31-37)
+            const uint32_t c = lenc[len_coder * 16 + ps] - 1;
+            lenc[len_coder * 16 + ps] = c;
+            LANE_FENCE();
+            if (c == 0) update_len_table(len_coder, ps);
+        }
     }
     FI void flush(uint32_t now_pos) {
-        if (eos) {   // WriteEndMarker (Encoder.java:818-835)
-            uint32_t ps = now_pos & ps_mask;
-            rc_bit(probs + E_IS_MATCH, (state << PBS) + ps, 1);
-            rc_bit(probs + E_IS_REP, state, 0);
-            state = st_match(state);
-            len_encode(0, 0, ps);
-            bt_enc(probs + E_PSLOT + (len_to_pos_state(kMatchMinLen) << 6), kNumPosSlotBits, 63);
-            uint32_t red = (1u << 30) - 1;
-            rc_direct(red >> kNumAlignBits, 30 - kNumAlignBits);
-            bt_rev_enc(probs + E_ALIGN, kNumAlignBits, red & kAlignMask);
-        }
+        if (eos) encode_symbol(0, kMatchMinLen, now_pos, prev_byte, 0, true);
+#pragma unroll 1
         for (int i = 0; i < 5; i++) shift_low();
         flush_out(outpos & ~(uint32_t)(kObuf - 1), outpos & (kObuf - 1));
     }
@@ -1068,13 +1147,7 @@ struct Enc {
         if (avail() == 0) { flush(0); return; }
         read_match_distances();
         DBG(1, 5);
-        rc_bit(probs + E_IS_MATCH, (state << PBS) + (now_pos & ps_mask), 0);
-        state = st_lit(state);
-        {
-            uint32_t cb = byte_at(0 - additional_offset);
-            lit_encode(lit_coder(now_pos, prev_byte), false, 0, cb);
-            prev_byte = cb;
-        }
+        encode_symbol(-1, 1, now_pos, byte_at(0 - additional_offset), 0, false);   // Encoder.java:860-878
         additional_offset--;
         now_pos++;
         if (avail() == 0) { flush(now_pos); return; }
@@ -1092,23 +1165,12 @@ struct Enc {
             DBG(4, len);
             if (bad || len == 0 || now_pos + len > n) { if (!bad) bad = 5; return; }
             PBEGIN(te);
-            uint32_t ps = now_pos & ps_mask;
-            uint32_t cs = (state << PBS) + ps;
-            if (len == 1 && back == -1) {
+            {
                 // both loads issued before the coder work (one round trip; out-of-range reads are 0)
-                const uint32_t cb = byte_at(0 - additional_offset);
+                const bool lit1 = len == 1 && back == -1;
+                const uint32_t cb = byte_at((lit1 ? 0 : (int32_t)len - 1) - additional_offset);
                 const uint32_t mb = byte_at((int32_t)(0 - rd0 - 1) - additional_offset);
-                rc_bit(probs + E_IS_MATCH, cs, 0);
-                uint16_t* sub = lit_coder(now_pos, prev_byte);
-                lit_encode(sub, !st_is_char(state), mb, cb);
-                prev_byte = cb;
-                state = st_lit(state);
-            } else {
-                const uint32_t last = byte_at((int32_t)len - 1 - additional_offset);
-                rc_bit(probs + E_IS_MATCH, cs, 1);
-                if (back < kNumRepDistances) encode_rep(back, len, ps, cs);
-                else encode_match(back, len, ps);
-                prev_byte = last;
+                encode_symbol(lit1 ? -1 : back, len, now_pos, cb, mb, false);
             }
             additional_offset -= (int32_t)len;
             now_pos += len;
@@ -1140,15 +1202,26 @@ __host__ __device__ inline uint32_t enc_lds_layout(const EncArgs& a, uint32_t* o
     return o;
 }
 
-template <typename PairT, bool LIT_LDS, int PBS>
-__global__ void __launch_bounds__(kWave) enc_kernel(EncArgs a) {
+// SPEC = 1: the level-5 parameters of bench.py (fb 32, lc 3, lp 0, pb 2, no end
+// marker) as compile-time constants; SPEC = 0: any parameters.
+template <typename PairT, bool LIT_LDS, int PBS, int SPEC>
+__global__ void __launch_bounds__(kWave, 4) enc_kernel(EncArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     Enc<PairT, LIT_LDS, PBS> e;
     e.lane = threadIdx.x;
-    e.fb = a.fb; e.lc = a.lc; e.lp = a.lp; e.pb = a.pb; e.ps_mask = (1u << a.pb) - 1; e.eos = a.eos;
-    e.dist_table_size = a.dist_table_size; e.tsize = a.len_table_size;
+    if (SPEC == 1) {
+        e.fb = 32; e.lc = 3; e.lp = 0; e.pb = 2; e.ps_mask = 3; e.eos = 0; e.tsize = 31;
+    } else {
+        e.fb = a.fb; e.lc = a.lc; e.lp = a.lp; e.pb = a.pb; e.ps_mask = (1u << a.pb) - 1; e.eos = a.eos;
+        e.tsize = a.len_table_size;
+    }
+    e.dist_table_size = a.dist_table_size;
     uint32_t off[L_COUNT];
-    enc_lds_layout(a, off);
+    {
+        EncArgs la = a;   // SPEC: the layout folds to constants (immediate LDS offsets, no SGPR per region)
+        if (SPEC == 1) { la.fb = 32; la.pb = 2; la.lc = 3; la.lp = 0; la.lit_in_lds = 0; la.pair_bytes = 4; la.len_table_size = 31; }
+        enc_lds_layout(la, off);
+    }
     e.pp = (uint16_t*)(smem + off[L_PP]);
     e.probs = (uint16_t*)(smem + off[L_PROBS]);
     e.lenp = (uint16_t*)(smem + off[L_LENP]);
@@ -1226,12 +1299,23 @@ uint32_t enc_lit_in_lds(const Derived& d) { return (d.lc + d.lp) <= (uint32_t)kL
 
 int enc_grid(const Derived&, int nstreams) { return nstreams; }   // one workgroup per stream
 
+template <typename PairT, bool LIT, int PBS, int SPEC>
+static void launch_spec(Ctx* ctx, const EncArgs& a, int grid, size_t lds, hipStream_t st) {
+    if (lds > 64 * 1024)
+        hipFuncSetAttribute((const void*)enc_kernel<PairT, LIT, PBS, SPEC>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    TimedLaunch tl(ctx, "enc_parse", st);
+    hipLaunchKernelGGL((enc_kernel<PairT, LIT, PBS, SPEC>), dim3(grid), dim3(kWave), lds, st, a);
+}
+
 template <typename PairT, bool LIT, int PBS>
 static void launch_one(Ctx* ctx, const EncArgs& a, int grid, size_t lds, hipStream_t st) {
-    if (lds > 64 * 1024)
-        hipFuncSetAttribute((const void*)enc_kernel<PairT, LIT, PBS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    TimedLaunch tl(ctx, "enc_parse", st);
-    hipLaunchKernelGGL((enc_kernel<PairT, LIT, PBS>), dim3(grid), dim3(kWave), lds, st, a);
+    if constexpr (std::is_same<PairT, uint32_t>::value && !LIT && PBS == 2) {
+        if (a.fb == 32 && a.lc == 3 && a.lp == 0 && a.pb == 2 && a.eos == 0) {
+            launch_spec<PairT, LIT, PBS, 1>(ctx, a, grid, lds, st);
+            return;
+        }
+    }
+    launch_spec<PairT, LIT, PBS, 0>(ctx, a, grid, lds, st);
 }
 
 template <typename PairT, bool LIT>

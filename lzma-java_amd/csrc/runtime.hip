@@ -200,7 +200,9 @@ static int encode_batch_dev(Ctx* ctx, const lzma_params* p, const uint8_t* d_in,
         int s1 = s0 + 1;
         // bytes bound the match-finder workspace; the stream count bounds the
         // per-workgroup parser scratch (one workgroup per stream)
-        while (s1 < nstreams && s1 - s0 < kMaxStreamsPerPass && h_offs[s1 + 1] - h_offs[s0] <= ctx->batch_bytes) s1++;
+        // the radix sorts and stream selection take an int item count: a pass stays below 2^31 bytes
+        const uint64_t pass_cap = std::min<uint64_t>(ctx->batch_bytes, (1ull << 31) - 1);
+        while (s1 < nstreams && s1 - s0 < kMaxStreamsPerPass && h_offs[s1 + 1] - h_offs[s0] <= pass_cap) s1++;
         int rc = encode_pass(ctx, d, d_in, h_offs, s0, s1, d_out, h_out_offs, h_out_lens, status.data(), st);
         if (rc) return rc;
         s0 = s1;
@@ -219,9 +221,12 @@ static int decode_batch_dev(Ctx* ctx, const uint8_t props[5], const uint8_t* d_i
     lzma_params p;
     if (lzma_read_props(props, &p) != LZMA_OK) return ctx->fail(LZMA_E_PARAM, "bad properties (Decoder.SetDecoderProperties false)");
     if (nstreams <= 0) return nstreams == 0 ? LZMA_OK : ctx->fail(LZMA_E_PARAM, "nstreams < 0");
+    for (int i = 0; i < nstreams; i++)   // the decoder kernel keeps 32-bit input positions
+        if (h_in_offs[i + 1] < h_in_offs[i] || h_in_offs[i + 1] - h_in_offs[i] >= 0xFFFFFFFFull)
+            return ctx->fail(LZMA_E_PARAM, "compressed stream %d: bad offsets or >= 4 GiB", i);
     uint32_t dict = (uint32_t)props[1] | ((uint32_t)props[2] << 8) | ((uint32_t)props[3] << 16) | ((uint32_t)props[4] << 24);
     const uint32_t lc = (uint32_t)p.lc, lp = (uint32_t)p.lp, pb = (uint32_t)p.pb;
-    const uint32_t lit_lds = (lc + lp) <= 3;
+    const uint32_t lit_lds = 0;   // literal coders always in the per-stream HBM scratch (dec.hip)
     std::vector<uint32_t> order(nstreams);
     std::iota(order.begin(), order.end(), 0u);
     std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
