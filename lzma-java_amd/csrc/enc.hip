@@ -44,6 +44,7 @@ constexpr int kGI = kGW / kWave;    // gather iterations per side (1 on hardware
 constexpr int kSides = 7;           // cur, rep0..rep3, pair0, pair1
 constexpr int kObuf = 256;          // output staging ring (bytes, power of two)
 constexpr int kLitSlots = (8 + kWave - 1) / kWave;   // literal bits per lane (1 on hardware)
+static_assert(kSides * kGW >= kNumFullDistances * 2, "tempPrices alias the gather window");
 
 #define FI __device__ __forceinline__
 // Lanes of one wavefront exchange data through LDS. The hardware runs one
@@ -101,6 +102,14 @@ FI uint32_t brev32(uint32_t v) {
 #endif
 }
 
+// GetPosSlot / GetPosSlot2 (Encoder.java:86-104) without the g_FastPos table:
+// 2 floor(log2 pos) plus the bit below the leading one (pos >= 2)
+FI uint32_t pos_slot(uint32_t pos) {
+    if (pos < 2) return pos;
+    const uint32_t n = 31u - (uint32_t)__clz((int)pos);
+    return (n << 1) | ((pos >> (n - 1)) & 1u);
+}
+
 FI uint32_t sel4(uint32_t i, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
     return i == 0 ? a : (i == 1 ? b : (i == 2 ? c : d));
 }
@@ -117,6 +126,8 @@ struct Enc {
     // ---- LDS
     uint16_t* pp;             // ProbPrices [512]
     uint16_t* probs;          // fixed models (lzma_common.h layout)
+    uint32_t* dmp;            // price cache of the decision models (isMatch .. isRep0Long, indices < E_PSLOT):
+                              // price0 | price1 << 16, rewritten by the coder whenever it adapts one
     uint16_t* lit;            // literal coders (LDS or HBM by LIT_LDS)
     uint16_t* lenp;           // [2][npos * tsize]
     uint32_t* lenc;           // [2][16]
@@ -134,6 +145,8 @@ struct Enc {
     int32_t* o_bp2;
     uint8_t* o_fs;
     uint32_t* o_backs;        // [4][kOptLds]
+    uint32_t* o_bytes;        // [kOptLds] cur byte | match byte << 8 | previous byte << 16 of each parsed
+                              // position, so the coder needs no HBM byte loads
     uint8_t* win;             // gather window [kSides][kGW]: cur side, reps 0-3, pairs 0-1
     uint8_t* obuf;            // output staging ring [kObuf]
     __amdgpu_buffer_rsrc_t spill;   // _optimum slots >= kOptLds in HBM (9 fields x kNumOpts dwords)
@@ -177,32 +190,36 @@ struct Enc {
     // The spill side goes through a buffer descriptor (buffer_load/store), an
     // access kind the compiler cannot merge with the LDS side into one generic
     // (flat) pointer. Byte offsets inside the per-block spill region:
-    //   price | pp | bp | bp2 | fs | backs[4], kNumOpts dwords each.
+    //   price | pp | bp | bp2 | fs | backs[4] | bytes, kNumOpts dwords each.
     FI uint32_t sload(uint32_t field, uint32_t i) const {
         return __builtin_amdgcn_raw_buffer_load_b32(spill, (field * kNumOpts + i) * 4, 0, 0);
     }
     FI void sstore(uint32_t field, uint32_t i, uint32_t v) {
         __builtin_amdgcn_raw_buffer_store_b32(v, spill, (field * kNumOpts + i) * 4, 0, 0);
     }
-    FI uint32_t price_at(uint32_t i) const { if (i < (uint32_t)kOptLds) return o_price[i]; return sload(0, i); }
-    FI void set_price(uint32_t i, uint32_t v) { if (i < (uint32_t)kOptLds) o_price[i] = v; else sstore(0, i, v); }
-    FI uint32_t pp_at(uint32_t i) const { if (i < (uint32_t)kOptLds) return o_pp[i]; return sload(1, i); }
-    FI void set_pp(uint32_t i, uint32_t v) { if (i < (uint32_t)kOptLds) o_pp[i] = v; else sstore(1, i, v); }
-    FI int32_t bp_at(uint32_t i) const { if (i < (uint32_t)kOptLds) return o_bp[i]; return (int32_t)sload(2, i); }
-    FI void set_bp(uint32_t i, int32_t v) { if (i < (uint32_t)kOptLds) o_bp[i] = v; else sstore(2, i, (uint32_t)v); }
-    FI int32_t bp2_at(uint32_t i) const { if (i < (uint32_t)kOptLds) return o_bp2[i]; return (int32_t)sload(3, i); }
-    FI void set_bp2(uint32_t i, int32_t v) { if (i < (uint32_t)kOptLds) o_bp2[i] = v; else sstore(3, i, (uint32_t)v); }
-    FI uint32_t fs_at(uint32_t i) const { if (i < (uint32_t)kOptLds) return (uint32_t)o_fs[i]; return sload(4, i); }
-    FI void set_fs(uint32_t i, uint32_t v) { if (i < (uint32_t)kOptLds) o_fs[i] = (uint8_t)v; else sstore(4, i, v); }
-    FI uint32_t back_at(uint32_t i, int k) const {
-        if (i < (uint32_t)kOptLds) return o_backs[k * kOptLds + i];
+    template <bool F = false> FI uint32_t price_at(uint32_t i) const { if (F || i < (uint32_t)kOptLds) return o_price[i]; return sload(0, i); }
+    template <bool F = false> FI void set_price(uint32_t i, uint32_t v) { if (F || i < (uint32_t)kOptLds) o_price[i] = v; else sstore(0, i, v); }
+    template <bool F = false> FI uint32_t pp_at(uint32_t i) const { if (F || i < (uint32_t)kOptLds) return o_pp[i]; return sload(1, i); }
+    template <bool F = false> FI void set_pp(uint32_t i, uint32_t v) { if (F || i < (uint32_t)kOptLds) o_pp[i] = v; else sstore(1, i, v); }
+    template <bool F = false> FI int32_t bp_at(uint32_t i) const { if (F || i < (uint32_t)kOptLds) return o_bp[i]; return (int32_t)sload(2, i); }
+    template <bool F = false> FI void set_bp(uint32_t i, int32_t v) { if (F || i < (uint32_t)kOptLds) o_bp[i] = v; else sstore(2, i, (uint32_t)v); }
+    template <bool F = false> FI int32_t bp2_at(uint32_t i) const { if (F || i < (uint32_t)kOptLds) return o_bp2[i]; return (int32_t)sload(3, i); }
+    template <bool F = false> FI void set_bp2(uint32_t i, int32_t v) { if (F || i < (uint32_t)kOptLds) o_bp2[i] = v; else sstore(3, i, (uint32_t)v); }
+    template <bool F = false> FI uint32_t fs_at(uint32_t i) const { if (F || i < (uint32_t)kOptLds) return (uint32_t)o_fs[i]; return sload(4, i); }
+    template <bool F = false> FI void set_fs(uint32_t i, uint32_t v) { if (F || i < (uint32_t)kOptLds) o_fs[i] = (uint8_t)v; else sstore(4, i, v); }
+    template <bool F = false> FI uint32_t back_at(uint32_t i, int k) const {
+        if (F || i < (uint32_t)kOptLds) return o_backs[k * kOptLds + i];
         return sload(5 + k, i);
     }
-    FI void set_back(uint32_t i, int k, uint32_t v) {
-        if (i < (uint32_t)kOptLds) o_backs[k * kOptLds + i] = v; else sstore(5 + k, i, v);
+    template <bool F = false> FI void set_back(uint32_t i, int k, uint32_t v) {
+        if (F || i < (uint32_t)kOptLds) o_backs[k * kOptLds + i] = v; else sstore(5 + k, i, v);
     }
-    FI uint32_t pos_prev(uint32_t i) const { return pp_at(i) & 0xFFFFu; }
-    FI uint32_t pos_prev2(uint32_t i) const { return pp_at(i) >> 16; }
+    template <bool F = false> FI uint32_t bytes_at(uint32_t i) const { if (F || i < (uint32_t)kOptLds) return o_bytes[i]; return sload(9, i); }
+    template <bool F = false> FI void set_bytes(uint32_t i, uint32_t v) { if (F || i < (uint32_t)kOptLds) o_bytes[i] = v; else sstore(9, i, v); }
+    // the gather window's bytes of the current position (see gather())
+    FI uint32_t win_bytes() const { return (uint32_t)win[1] | ((uint32_t)win[kGW + 1] << 8) | ((uint32_t)win[0] << 16); }
+    template <bool F = false> FI uint32_t pos_prev(uint32_t i) const { return pp_at<F>(i) & 0xFFFFu; }
+    template <bool F = false> FI uint32_t pos_prev2(uint32_t i) const { return pp_at<F>(i) >> 16; }
     // after lanes wrote slots up to `hi`, make them visible to every lane
     FI void fence_upto(uint32_t hi) {
         LANE_FENCE();
@@ -213,6 +230,10 @@ struct Enc {
     FI uint32_t price_bit(uint32_t prob, uint32_t bit) const { return pp[(((prob - bit) ^ (0u - bit)) & 2047u) >> 2]; }
     FI uint32_t price0(uint32_t prob) const { return pp[prob >> 2]; }
     FI uint32_t price1(uint32_t prob) const { return pp[(kBitModelTotal - prob) >> 2]; }
+    // one LDS read per decision price (no prob -> ProbPrices chain)
+    FI uint32_t dm0(uint32_t i) const { return dmp[i] & 0xFFFFu; }
+    FI uint32_t dm1(uint32_t i) const { return dmp[i] >> 16; }
+    FI uint32_t dmb(uint32_t i, uint32_t bit) const { return bit ? dm1(i) : dm0(i); }
     FI uint32_t bt_price(const uint16_t* p, int nbits, uint32_t sym) const {   // BitTreeEncoder.java:38-48
         uint32_t price = 0, m = 1;
         for (int b = nbits; b != 0;) { b--; uint32_t bit = (sym >> b) & 1; price += price_bit(p[m], bit); m = (m << 1) + bit; }
@@ -241,12 +262,23 @@ struct Enc {
             uint32_t ctx = (0x100u | sym) >> (i + 1);
             uint32_t idx = ctx;
             if (match_mode && i >= first) idx = ((1 + ((mb >> i) & 1)) << 8) + ctx;
+#ifdef LZG_ABL_LITLOAD
+            price += price_bit(1024u + (idx & 7u), bit);   // ablation: no literal-model load
+#else
             price += price_bit(p[idx], bit);
+#endif
         }
+#if LZG_WAVE == 64
+        // sum of lanes 0-7 without LDS traffic: DPP quad swaps, then a rotate by 4
+        // within the 16-lane row; lane 0 holds the total (readlane keeps it scalar)
+        price += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)price, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+        price += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)price, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+        price += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)price, 0x12C, 0xF, 0xF, false);  // row_ror:12 (lane i reads lane i+4)
+        return (uint32_t)__builtin_amdgcn_readlane((int)price, 0);
+#else
         for (int o = 1; o < 8 && o < kWave; o <<= 1) price += __shfl_xor(price, o);
-        // readfirstlane (not a shuffle): the result is provably wave-uniform, so
-        // the compiler keeps every price comparison downstream a scalar branch
         return (uint32_t)__builtin_amdgcn_readfirstlane((int)price);
+#endif
     }
     FI uint32_t len_price(int which, uint32_t sym, uint32_t ps) const {
         return lenp[(which << pb) * tsize + ps * tsize + sym];
@@ -494,8 +526,15 @@ struct Enc {
         for (int t = 0; t < kQS; t++) {
             const uint32_t p = pr[t];
             const uint16_t np = (uint16_t)(q.bit[t] ? p - (p >> kNumMoveBits) : p + ((kBitModelTotal - p) >> kNumMoveBits));
+#ifdef LZG_ABL_LITSTORE
+            if (q.kind[t] == QK_LIT) {}   // ablation: literal models never adapt
+#else
             if (q.kind[t] == QK_LIT) lit[q.idx[t]] = np;
-            else if (q.kind[t] == QK_PROB) probs[q.idx[t]] = np;
+#endif
+            else if (q.kind[t] == QK_PROB) {
+                probs[q.idx[t]] = np;
+                if (q.idx[t] < (uint32_t)E_PSLOT) dmp[q.idx[t]] = price0(np) | (price1(np) << 16);
+            }
         }
         LANE_FENCE();
     }
@@ -518,7 +557,7 @@ struct Enc {
     }
     FI void fill_distances_prices() {   // Encoder.java:1087-1118
         LANE_FOR(uint32_t, i, (uint32_t)kStartPosModelIndex, (uint32_t)kNumFullDistances) {
-            uint32_t ps = c_tab.fastpos[i], footer = (ps >> 1) - 1, base = (2 | (ps & 1)) << footer;
+            uint32_t ps = pos_slot(i), footer = (ps >> 1) - 1, base = (2 | (ps & 1)) << footer;
             tp[i] = (uint16_t)rev_price(probs + E_PENC + (int32_t)(base - ps - 1), (int)footer, i - base);
         }
         for (uint32_t l = 0; l < (uint32_t)kNumLenToPosStates; l++) {
@@ -533,7 +572,7 @@ struct Enc {
         for (uint32_t l = 0; l < (uint32_t)kNumLenToPosStates; l++) {
             uint32_t st = l << kNumPosSlotBits, st2 = l * kNumFullDistances;
             LANE_FOR(uint32_t, i, 0u, (uint32_t)kNumFullDistances)
-                dp[st2 + i] = (uint16_t)(i < (uint32_t)kStartPosModelIndex ? psp[st + i] : psp[st + c_tab.fastpos[i]] + tp[i]);
+                dp[st2 + i] = (uint16_t)(i < (uint32_t)kStartPosModelIndex ? psp[st + i] : psp[st + pos_slot(i)] + tp[i]);
         }
         match_price_count = 0;
         LANE_FENCE();
@@ -587,17 +626,17 @@ struct Enc {
         if (num > 0) { mfpos += num; additional_offset += (int32_t)num; }
     }
     FI uint32_t rep_len1_price(uint32_t st, uint32_t ps) const {
-        return price0(probs[E_G0 + st]) + price0(probs[E_R0L + (st << PBS) + ps]);
+        return dm0(E_G0 + st) + dm0(E_R0L + (st << PBS) + ps);
     }
     FI uint32_t pure_rep_price(uint32_t ri, uint32_t st, uint32_t ps) const {
         uint32_t price;
         if (ri == 0) {
-            price = price0(probs[E_G0 + st]);
-            price += price1(probs[E_R0L + (st << PBS) + ps]);
+            price = dm0(E_G0 + st);
+            price += dm1(E_R0L + (st << PBS) + ps);
         } else {
-            price = price1(probs[E_G0 + st]);
-            if (ri == 1) price += price0(probs[E_G1 + st]);
-            else { price += price1(probs[E_G1 + st]); price += price_bit(probs[E_G2 + st], ri - 2); }
+            price = dm1(E_G0 + st);
+            if (ri == 1) price += dm0(E_G1 + st);
+            else { price += dm1(E_G1 + st); price += dmb(E_G2 + st, ri - 2); }
         }
         return price;
     }
@@ -607,11 +646,7 @@ struct Enc {
     FI uint32_t dist_price(uint32_t pos, uint32_t len) const {   // GetPosLenPrice without the length part
         uint32_t lps = len_to_pos_state(len);
         if (pos < (uint32_t)kNumFullDistances) return (uint32_t)dp[lps * kNumFullDistances + pos];
-        uint32_t slot2;
-        if (pos < (1u << 17)) slot2 = c_tab.fastpos[pos >> 6] + 12;
-        else if (pos < (1u << 27)) slot2 = c_tab.fastpos[pos >> 16] + 32;
-        else slot2 = c_tab.fastpos[pos >> 26] + 52;
-        return (uint32_t)psp[(lps << kNumPosSlotBits) + slot2] + ap[pos & kAlignMask];
+        return (uint32_t)psp[(lps << kNumPosSlotBits) + pos_slot(pos)] + ap[pos & kAlignMask];
     }
     FI uint32_t pos_len_price(uint32_t pos, uint32_t len, uint32_t ps) const {   // Encoder.java:323-333
         return dist_price(pos, len) + len_price(0, len - kMatchMinLen, ps);
@@ -619,6 +654,12 @@ struct Enc {
     // while (lenEnd < target) _optimum[++lenEnd].Price = kIfinityPrice
     FI void extend_to(uint32_t& len_end, uint32_t target) {
         if (len_end >= target) return;
+        if (target < (uint32_t)kOptLds) {
+            LANE_FOR(uint32_t, i, len_end + 1, target + 1) set_price<true>(i, kInfinityPrice);
+            len_end = target;
+            LANE_FENCE();
+            return;
+        }
         LANE_FOR(uint32_t, i, len_end + 1, target + 1) set_price(i, kInfinityPrice);
         len_end = target;
         fence_upto(target);
@@ -680,79 +721,91 @@ struct Enc {
         fence_upto(base_slot + hi);
     }
     // uniform single-slot update for the two-step (x + literal + rep0) candidates
-    FI void relax_two_step(uint32_t s, uint32_t cl, uint32_t pos_prev_v, bool prev2, uint32_t pos_prev2_v, int32_t back2) {
-        if (cl < price_at(s)) {
-            set_price(s, cl);
-            set_bp(s, 0);
+    template <bool F> FI void relax_two_step_t(uint32_t s, uint32_t cl, uint32_t pos_prev_v, bool prev2, uint32_t pos_prev2_v, int32_t back2) {
+        if (cl < price_at<F>(s)) {
+            set_price<F>(s, cl);
+            set_bp<F>(s, 0);
             if (prev2) {
-                set_pp(s, pos_prev_v | (pos_prev2_v << 16));
-                set_fs(s, (fs_at(s) & ~3u) | 3u);
-                set_bp2(s, back2);
+                set_pp<F>(s, pos_prev_v | (pos_prev2_v << 16));
+                set_fs<F>(s, (fs_at<F>(s) & ~3u) | 3u);
+                set_bp2<F>(s, back2);
             } else {
-                set_pp(s, (pp_at(s) & 0xFFFF0000u) | pos_prev_v);
-                set_fs(s, (fs_at(s) & ~3u) | 1u);
+                set_pp<F>(s, (pp_at<F>(s) & 0xFFFF0000u) | pos_prev_v);
+                set_fs<F>(s, (fs_at<F>(s) & ~3u) | 1u);
             }
         }
         fence_upto(s);
     }
 
-    FI uint32_t backward(int32_t* back_res, uint32_t cur) {   // Encoder.java:335-362
+    FI void relax_two_step(uint32_t s, uint32_t cl, uint32_t pos_prev_v, bool prev2, uint32_t pos_prev2_v, int32_t back2) {
+        if (s < (uint32_t)kOptLds) relax_two_step_t<true>(s, cl, pos_prev_v, prev2, pos_prev2_v, back2);
+        else relax_two_step_t<false>(s, cl, pos_prev_v, prev2, pos_prev2_v, back2);
+    }
+
+    template <bool F> FI uint32_t backward_t(int32_t* back_res, uint32_t cur) {   // Encoder.java:335-362
         PBEGIN(tb);
         opt_end = (int32_t)cur;
-        uint32_t pos_mem = pos_prev(cur);
-        int32_t back_mem = bp_at(cur);
+        uint32_t pos_mem = pos_prev<F>(cur);
+        int32_t back_mem = bp_at<F>(cur);
         uint32_t guard = 0;
         do {
             if (++guard > (uint32_t)kNumOpts || pos_mem >= cur) { bad = 2; break; }
-            uint32_t fsc = fs_at(cur);
+            uint32_t fsc = fs_at<F>(cur);
             if (fsc & 1u) {
-                set_bp(pos_mem, -1);
-                set_fs(pos_mem, fs_at(pos_mem) & ~1u);
-                set_pp(pos_mem, (pp_at(pos_mem) & 0xFFFF0000u) | (pos_mem - 1));
+                set_bp<F>(pos_mem, -1);
+                set_fs<F>(pos_mem, fs_at<F>(pos_mem) & ~1u);
+                set_pp<F>(pos_mem, (pp_at<F>(pos_mem) & 0xFFFF0000u) | (pos_mem - 1));
                 if (fsc & 2u) {
                     uint32_t m1 = pos_mem - 1;
-                    set_fs(m1, fs_at(m1) & ~1u);
-                    set_pp(m1, (pp_at(m1) & 0xFFFF0000u) | pos_prev2(cur));
-                    set_bp(m1, bp2_at(cur));
+                    set_fs<F>(m1, fs_at<F>(m1) & ~1u);
+                    set_pp<F>(m1, (pp_at<F>(m1) & 0xFFFF0000u) | pos_prev2<F>(cur));
+                    set_bp<F>(m1, bp2_at<F>(cur));
                 }
             }
             uint32_t ppv = pos_mem;
             int32_t back_cur = back_mem;
-            back_mem = bp_at(ppv);
-            pos_mem = pos_prev(ppv);
-            set_bp(ppv, back_cur);
-            set_pp(ppv, (pp_at(ppv) & 0xFFFF0000u) | cur);
+            back_mem = bp_at<F>(ppv);
+            pos_mem = pos_prev<F>(ppv);
+            set_bp<F>(ppv, back_cur);
+            set_pp<F>(ppv, (pp_at<F>(ppv) & 0xFFFF0000u) | cur);
             cur = ppv;
         } while (cur > 0);
-        opt_cur = (int32_t)pos_prev(0);
-        *back_res = bp_at(0);
+        opt_cur = (int32_t)pos_prev<F>(0);
+        *back_res = bp_at<F>(0);
         PEND(PF_BACK, tb);
         return (uint32_t)opt_cur;
     }
 
+    FI uint32_t backward(int32_t* back_res, uint32_t cur) {   // every slot touched is <= cur
+        return cur < (uint32_t)kOptLds ? backward_t<true>(back_res, cur) : backward_t<false>(back_res, cur);
+    }
+
     // getOptimum (Encoder.java:364-811). Returns length; *back_res = pos.
-    FI uint32_t get_optimum(uint32_t position, int32_t* back_res) {
+    FI uint32_t get_optimum(uint32_t position, int32_t* back_res, uint32_t* sym_slot) {
         if (opt_end != opt_cur) {
             uint32_t c = (uint32_t)opt_cur;
-            uint32_t nxt = pos_prev(c);
-            *back_res = bp_at(c);
+            *sym_slot = c;
+            uint32_t nxt;
+            if (c < (uint32_t)kOptLds) { nxt = pos_prev<true>(c); *back_res = bp_at<true>(c); }
+            else { nxt = pos_prev(c); *back_res = bp_at(c); }
             opt_cur = (int32_t)nxt;
             if (nxt <= c || nxt > (uint32_t)opt_end) { bad = 3; return 1; }
             return nxt - c;
         }
         opt_cur = opt_end = 0;
+        *sym_slot = 0;
         uint32_t len_main;
         if (longest_found) { len_main = longest_len; longest_found = 0; }
         else len_main = read_match_distances();
         uint32_t npairs = num_pairs;
-        uint32_t num_avail = avail() + 1;
-        if (num_avail < 2) { *back_res = -1; return 1; }
-        if (num_avail > (uint32_t)kMatchMaxLen) num_avail = kMatchMaxLen;
-
         rp0 = rd0; rp1 = rd1; rp2 = rd2; rp3 = rd3;
         PCOUNT(PF_NOPT);
         PBEGIN(t0);
         gather(false);
+        set_bytes(0, win_bytes());
+        uint32_t num_avail = avail() + 1;
+        if (num_avail < 2) { *back_res = -1; LANE_FENCE(); return 1; }
+        if (num_avail > (uint32_t)kMatchMaxLen) num_avail = kMatchMaxLen;
         uint32_t rl0 = glen(gm0, rp0, 0, kMatchMaxLen);
         uint32_t rl1 = glen(gm1, rp1, 0, kMatchMaxLen);
         uint32_t rl2 = glen(gm2, rp2, 0, kMatchMaxLen);
@@ -779,11 +832,11 @@ struct Enc {
         set_fs(0, (fs_at(0) & 0xFu) | (state << 4));
         uint32_t pos_state = position & ps_mask;
         PBEGIN(t1);
-        uint32_t p1 = price0(probs[E_IS_MATCH + (state << PBS) + pos_state]) +
-                      lit_price(lit_coder(position, prev_byte), !st_is_char(state), match_byte, cur_byte);
+        uint32_t p1 = dm0(E_IS_MATCH + (state << PBS) + pos_state) +
+                      lit_price(lit_coder(position, a_byte(-1)), !st_is_char(state), match_byte, cur_byte);
         PEND(PF_LIT, t1);
-        uint32_t match_price = price1(probs[E_IS_MATCH + (state << PBS) + pos_state]);
-        uint32_t rep_match_price = match_price + price1(probs[E_IS_REP + state]);
+        uint32_t match_price = dm1(E_IS_MATCH + (state << PBS) + pos_state);
+        uint32_t rep_match_price = match_price + dm1(E_IS_REP + state);
         int32_t bp1 = -1;
         if (match_byte == cur_byte) {
             uint32_t srp = rep_match_price + rep_len1_price(state, pos_state);
@@ -806,7 +859,7 @@ struct Enc {
             if (rl < 2) continue;
             relax_rep(0, 2, rl, rep_match_price + pure_rep_price(i, state, pos_state), pos_state, 0, i);
         }
-        uint32_t normal_match_price = match_price + price0(probs[E_IS_REP + state]);
+        uint32_t normal_match_price = match_price + dm0(E_IS_REP + state);
         uint32_t lstart = rl0 >= 2 ? rl0 + 1 : 2;
         if (lstart <= len_main) {
             // no look-ahead in this loop: every length is independent
@@ -828,6 +881,93 @@ struct Enc {
         return parse_forward(position, back_res, len_end);
     }
 
+    // Position step of getOptimum's forward loop (Encoder.java:685-742): the state
+    // and reps of cur from its best path, the literal and short-rep candidates
+    // of cur + 1. F: every slot touched (<= cur + 1) is below kOptLds, so the
+    // slot accesses are plain LDS operations (no spill branches, and no wait on
+    // outstanding HBM operations merged into them).
+    template <bool F>
+    FI bool pos_step(uint32_t cur, uint32_t position, uint32_t& st, uint32_t& pos_state, uint32_t& cur_and1,
+                     uint32_t& match_price, uint32_t& rep_match_price, uint32_t& cur_byte, uint32_t& match_byte) {
+        PBEGIN(ts);
+        uint32_t ppc = pp_at<F>(cur);
+        uint32_t pos_prev_c = ppc & 0xFFFFu;
+        uint32_t fsc = fs_at<F>(cur);
+        int32_t bpc = bp_at<F>(cur);
+        uint32_t pprev = pos_prev_c;
+        if (fsc & 1u) {
+            pprev--;
+            if (fsc & 2u) {
+                st = fs_at<F>(ppc >> 16) >> 4;
+                if (bp2_at<F>(cur) < kNumRepDistances) st = st_long(st);
+                else st = st_match(st);
+            } else st = fs_at<F>(pprev) >> 4;
+            st = st_lit(st);
+        } else st = fs_at<F>(pprev) >> 4;
+        if (pprev == cur - 1) {
+            if (bpc == 0) st = st_short(st);
+            else st = st_lit(st);
+        } else {
+            int32_t pos;
+            if ((fsc & 1u) && (fsc & 2u)) {
+                pprev = ppc >> 16;
+                pos = bp2_at<F>(cur);
+                st = st_long(st);
+            } else {
+                pos = bpc;
+                if (pos < kNumRepDistances) st = st_long(st);
+                else st = st_match(st);
+            }
+            uint32_t b0 = back_at<F>(pprev, 0), b1 = back_at<F>(pprev, 1), b2 = back_at<F>(pprev, 2), b3 = back_at<F>(pprev, 3);
+            if (pos < kNumRepDistances) {
+                if (pos == 0) { rp0 = b0; rp1 = b1; rp2 = b2; rp3 = b3; }
+                else if (pos == 1) { rp0 = b1; rp1 = b0; rp2 = b2; rp3 = b3; }
+                else if (pos == 2) { rp0 = b2; rp1 = b0; rp2 = b1; rp3 = b3; }
+                else { rp0 = b3; rp1 = b0; rp2 = b1; rp3 = b2; }
+            } else {
+                rp0 = (uint32_t)(pos - kNumRepDistances); rp1 = b0; rp2 = b1; rp3 = b2;
+            }
+        }
+        set_fs<F>(cur, (fsc & 0xFu) | (st << 4));
+        set_back<F>(cur, 0, rp0); set_back<F>(cur, 1, rp1); set_back<F>(cur, 2, rp2); set_back<F>(cur, 3, rp3);
+        uint32_t cur_price = price_at<F>(cur);
+        pos_state = position & ps_mask;
+        PEND(PF_STATE, ts);
+        PBEGIN(tg);
+        gather(true);
+        set_bytes<F>(cur, win_bytes());
+        PEND(PF_REPLEN, tg);
+        cur_byte = a_byte(0);
+        match_byte = b_byte(1, rp0, 0);
+        PBEGIN(tl);
+        cur_and1 = cur_price + dm0(E_IS_MATCH + (st << PBS) + pos_state) +
+                            lit_price(lit_coder(position, a_byte(-1)), !st_is_char(st), match_byte, cur_byte);
+        PEND(PF_LIT, tl);
+        PBEGIN(tn);
+        uint32_t nx = cur + 1;
+        bool next_is_char = false;
+        uint32_t nx_price = price_at<F>(nx);
+        uint32_t nx_pp = pp_at<F>(nx);
+        int32_t nx_bp = bp_at<F>(nx);
+        if (cur_and1 < nx_price) {
+            nx_price = cur_and1; nx_pp = (nx_pp & 0xFFFF0000u) | cur; nx_bp = -1;
+            set_price<F>(nx, nx_price); set_pp<F>(nx, nx_pp); set_bp<F>(nx, -1); set_fs<F>(nx, fs_at<F>(nx) & ~1u);
+            next_is_char = true;
+        }
+        match_price = cur_price + dm1(E_IS_MATCH + (st << PBS) + pos_state);
+        rep_match_price = match_price + dm1(E_IS_REP + st);
+        if (match_byte == cur_byte && !((nx_pp & 0xFFFFu) < cur && nx_bp == 0)) {
+            uint32_t srp = rep_match_price + rep_len1_price(st, pos_state);
+            if (srp <= nx_price) {
+                set_price<F>(nx, srp); set_pp<F>(nx, (nx_pp & 0xFFFF0000u) | cur); set_bp<F>(nx, 0); set_fs<F>(nx, fs_at<F>(nx) & ~1u);
+                next_is_char = true;
+            }
+        }
+        fence_upto(nx);
+        PEND(PF_STATE, tn);
+        return next_is_char;
+    }
+
     FI uint32_t parse_forward(uint32_t position, int32_t* back_res, uint32_t len_end) {
         uint32_t cur = 0;
         DBG(5, len_end);
@@ -847,82 +987,12 @@ struct Enc {
                 return backward(back_res, cur);
             }
             position++;
-            PBEGIN(ts);
-            uint32_t ppc = pp_at(cur);
-            uint32_t pos_prev_c = ppc & 0xFFFFu;
-            uint32_t fsc = fs_at(cur);
-            int32_t bpc = bp_at(cur);
-            uint32_t st;
-            uint32_t pprev = pos_prev_c;
-            if (fsc & 1u) {
-                pprev--;
-                if (fsc & 2u) {
-                    st = fs_at(ppc >> 16) >> 4;
-                    if (bp2_at(cur) < kNumRepDistances) st = st_long(st);
-                    else st = st_match(st);
-                } else st = fs_at(pprev) >> 4;
-                st = st_lit(st);
-            } else st = fs_at(pprev) >> 4;
-            if (pprev == cur - 1) {
-                if (bpc == 0) st = st_short(st);
-                else st = st_lit(st);
-            } else {
-                int32_t pos;
-                if ((fsc & 1u) && (fsc & 2u)) {
-                    pprev = ppc >> 16;
-                    pos = bp2_at(cur);
-                    st = st_long(st);
-                } else {
-                    pos = bpc;
-                    if (pos < kNumRepDistances) st = st_long(st);
-                    else st = st_match(st);
-                }
-                uint32_t b0 = back_at(pprev, 0), b1 = back_at(pprev, 1), b2 = back_at(pprev, 2), b3 = back_at(pprev, 3);
-                if (pos < kNumRepDistances) {
-                    if (pos == 0) { rp0 = b0; rp1 = b1; rp2 = b2; rp3 = b3; }
-                    else if (pos == 1) { rp0 = b1; rp1 = b0; rp2 = b2; rp3 = b3; }
-                    else if (pos == 2) { rp0 = b2; rp1 = b0; rp2 = b1; rp3 = b3; }
-                    else { rp0 = b3; rp1 = b0; rp2 = b1; rp3 = b2; }
-                } else {
-                    rp0 = (uint32_t)(pos - kNumRepDistances); rp1 = b0; rp2 = b1; rp3 = b2;
-                }
-            }
-            set_fs(cur, (fsc & 0xFu) | (st << 4));
-            set_back(cur, 0, rp0); set_back(cur, 1, rp1); set_back(cur, 2, rp2); set_back(cur, 3, rp3);
-            uint32_t cur_price = price_at(cur);
-            uint32_t pos_state = position & ps_mask;
-            PEND(PF_STATE, ts);
-            PBEGIN(tg);
-            gather(true);
-            PEND(PF_REPLEN, tg);
-            uint32_t cur_byte = a_byte(0);
-            uint32_t match_byte = b_byte(1, rp0, 0);
-            PBEGIN(tl);
-            uint32_t cur_and1 = cur_price + price0(probs[E_IS_MATCH + (st << PBS) + pos_state]) +
-                                lit_price(lit_coder(position, a_byte(-1)), !st_is_char(st), match_byte, cur_byte);
-            PEND(PF_LIT, tl);
-            PBEGIN(tn);
-            uint32_t nx = cur + 1;
-            bool next_is_char = false;
-            uint32_t nx_price = price_at(nx);
-            uint32_t nx_pp = pp_at(nx);
-            int32_t nx_bp = bp_at(nx);
-            if (cur_and1 < nx_price) {
-                nx_price = cur_and1; nx_pp = (nx_pp & 0xFFFF0000u) | cur; nx_bp = -1;
-                set_price(nx, nx_price); set_pp(nx, nx_pp); set_bp(nx, -1); set_fs(nx, fs_at(nx) & ~1u);
-                next_is_char = true;
-            }
-            uint32_t match_price = cur_price + price1(probs[E_IS_MATCH + (st << PBS) + pos_state]);
-            uint32_t rep_match_price = match_price + price1(probs[E_IS_REP + st]);
-            if (match_byte == cur_byte && !((nx_pp & 0xFFFFu) < cur && nx_bp == 0)) {
-                uint32_t srp = rep_match_price + rep_len1_price(st, pos_state);
-                if (srp <= nx_price) {
-                    set_price(nx, srp); set_pp(nx, (nx_pp & 0xFFFF0000u) | cur); set_bp(nx, 0); set_fs(nx, fs_at(nx) & ~1u);
-                    next_is_char = true;
-                }
-            }
-            fence_upto(nx);
-            PEND(PF_STATE, tn);
+            uint32_t st, pos_state, cur_and1, match_price, rep_match_price, cur_byte, match_byte;
+            // every slot the step touches is <= cur + 1: LDS only when that is below kOptLds
+            const bool next_is_char =
+                cur + 1 < (uint32_t)kOptLds
+                    ? pos_step<true>(cur, position, st, pos_state, cur_and1, match_price, rep_match_price, cur_byte, match_byte)
+                    : pos_step<false>(cur, position, st, pos_state, cur_and1, match_price, rep_match_price, cur_byte, match_byte);
             uint32_t num_avail_full = avail() + 1;
             if ((uint32_t)kNumOpts - 1 - cur < num_avail_full) num_avail_full = kNumOpts - 1 - cur;
             uint32_t num_avail = num_avail_full;
@@ -937,7 +1007,7 @@ struct Enc {
                     PBEGIN(t2b);
                     uint32_t st2 = st_lit(st);
                     uint32_t psn = (position + 1) & ps_mask;
-                    uint32_t nrmp = cur_and1 + price1(probs[E_IS_MATCH + (st2 << PBS) + psn]) + price1(probs[E_IS_REP + st2]);
+                    uint32_t nrmp = cur_and1 + dm1(E_IS_MATCH + (st2 << PBS) + psn) + dm1(E_IS_REP + st2);
                     uint32_t offset = cur + 1 + lt2;
                     extend_to(len_end, offset);
                     relax_two_step(offset, nrmp + rep_price(0, lt2, st2, psn), cur + 1, false, 0, 0);
@@ -969,12 +1039,12 @@ struct Enc {
                         uint32_t st2 = st_long(st);
                         uint32_t psn = (position + lt) & ps_mask;
                         uint32_t clcp = rep_match_price + rep_price(ri, lt, st, pos_state) +
-                                        price0(probs[E_IS_MATCH + (st2 << PBS) + psn]) +
+                                        dm0(E_IS_MATCH + (st2 << PBS) + psn) +
                                         lit_price(lit_coder(position + lt, a_byte((int32_t)lt - 1)), true,
                                                   b_byte(1 + (int)ri, rdist, (int32_t)lt), a_byte((int32_t)lt));
                         st2 = st_lit(st2);
                         psn = (position + lt + 1) & ps_mask;
-                        uint32_t nrmp = clcp + price1(probs[E_IS_MATCH + (st2 << PBS) + psn]) + price1(probs[E_IS_REP + st2]);
+                        uint32_t nrmp = clcp + dm1(E_IS_MATCH + (st2 << PBS) + psn) + dm1(E_IS_REP + st2);
                         uint32_t offset = lt + 1 + lt2;
                         extend_to(len_end, cur + offset);
                         relax_two_step(cur + offset, nrmp + rep_price(0, lt2, st2, psn), cur + lt + 1, true, cur, (int32_t)ri);
@@ -994,7 +1064,7 @@ struct Enc {
 #ifdef LZG_PROF
                 uint64_t tm = PCLK();
 #endif
-                uint32_t normal_match_price = match_price + price0(probs[E_IS_REP + st]);
+                uint32_t normal_match_price = match_price + dm0(E_IS_REP + st);
                 extend_to(len_end, cur + new_len);
                 uint32_t offs = 0;
                 while (offs + 1 < npairs && start_len > md_len[offs]) offs++;
@@ -1022,12 +1092,12 @@ struct Enc {
                             uint32_t cl = normal_match_price + pos_len_price(cur_back, lt, pos_state);
                             uint32_t st2 = st_match(st);
                             uint32_t psn = (position + lt) & ps_mask;
-                            uint32_t clcp = cl + price0(probs[E_IS_MATCH + (st2 << PBS) + psn]) +
+                            uint32_t clcp = cl + dm0(E_IS_MATCH + (st2 << PBS) + psn) +
                                             lit_price(lit_coder(position + lt, a_byte((int32_t)lt - 1)), true,
                                                       b_byte(side, cur_back, (int32_t)lt), a_byte((int32_t)lt));
                             st2 = st_lit(st2);
                             psn = (position + lt + 1) & ps_mask;
-                            uint32_t nrmp = clcp + price1(probs[E_IS_MATCH + (st2 << PBS) + psn]) + price1(probs[E_IS_REP + st2]);
+                            uint32_t nrmp = clcp + dm1(E_IS_MATCH + (st2 << PBS) + psn) + dm1(E_IS_REP + st2);
                             uint32_t offset = lt + 1 + lt2;
                             extend_to(len_end, cur + offset);
                             relax_two_step(cur + offset, nrmp + rep_price(0, lt2, st2, psn), cur + lt + 1, true, cur,
@@ -1081,11 +1151,7 @@ struct Enc {
                 q_len(q, 0, len - kMatchMinLen, ps);
                 len_coder = 0;
                 const uint32_t pos = eos_marker ? 0xFFFFFFFFu : (uint32_t)(back - kNumRepDistances);
-                uint32_t slot;
-                if (eos_marker) slot = 63;
-                else if (pos < (1u << 11)) slot = c_tab.fastpos[pos];
-                else if (pos < (1u << 21)) slot = c_tab.fastpos[pos >> 10] + 20;
-                else slot = c_tab.fastpos[pos >> 20] + 40;
+                const uint32_t slot = eos_marker ? 63u : pos_slot(pos);
                 q_bt(q, E_PSLOT + (len_to_pos_state(len) << 6), kNumPosSlotBits, slot);
                 if (slot >= (uint32_t)kStartPosModelIndex) {
                     const uint32_t footer = (slot >> 1) - 1, base = (2 | (slot & 1)) << footer, red = pos - base;
@@ -1122,6 +1188,7 @@ struct Enc {
 #endif
         const uint32_t nlit = 0x300u << (lc + lp);
         LANE_FOR(uint32_t, i, 0u, (uint32_t)E_COUNT) probs[i] = kBitModelTotal >> 1;
+        LANE_FOR(uint32_t, i, 0u, (uint32_t)E_PSLOT) dmp[i] = price0(kBitModelTotal >> 1) | (price1(kBitModelTotal >> 1) << 16);
         LANE_FOR(uint32_t, i, 0u, nlit) lit[i] = kBitModelTotal >> 1;
         LANE_FOR(uint32_t, i, 0u, 256u) psp[i] = 0;
         if (!LIT_LDS) SPILL_FENCE();
@@ -1160,17 +1227,27 @@ struct Enc {
 #ifdef LZG_PROF
             const uint64_t tg = PCLK();
 #endif
-            uint32_t len = get_optimum(now_pos, &back);
+            uint32_t sym_slot;
+            uint32_t len = get_optimum(now_pos, &back, &sym_slot);
             PEND(PF_GETOPT, tg);
             DBG(4, len);
             if (bad || len == 0 || now_pos + len > n) { if (!bad) bad = 5; return; }
             PBEGIN(te);
-            {
-                // both loads issued before the coder work (one round trip; out-of-range reads are 0)
-                const bool lit1 = len == 1 && back == -1;
-                const uint32_t cb = byte_at((lit1 ? 0 : (int32_t)len - 1) - additional_offset);
-                const uint32_t mb = byte_at((int32_t)(0 - rd0 - 1) - additional_offset);
-                encode_symbol(lit1 ? -1 : back, len, now_pos, cb, mb, false);
+            if (len == 1 && back == -1) {
+                // literal: its byte, match byte and previous byte were recorded when the
+                // position was parsed (o_bytes); a rep or match codes no byte
+                // The match byte was taken with the rep0 of the slot's own best path; a
+                // two-step candidate's middle literal can sit on a path with another rep0
+                // (then the byte is re-read). Slot 0 always used the current rep0.
+                const bool fs_ = sym_slot < (uint32_t)kOptLds;
+                const uint32_t b = fs_ ? bytes_at<true>(sym_slot) : bytes_at(sym_slot);
+                const uint32_t r0 = fs_ ? back_at<true>(sym_slot, 0) : back_at(sym_slot, 0);
+                prev_byte = b >> 16;
+                uint32_t mb = (b >> 8) & 0xFFu;
+                if (sym_slot != 0 && r0 != rd0) mb = byte_at((int32_t)(0 - rd0 - 1) - additional_offset);
+                encode_symbol(-1, 1, now_pos, b & 0xFFu, mb, false);
+            } else {
+                encode_symbol(back, len, now_pos, 0, 0, false);
             }
             additional_offset -= (int32_t)len;
             now_pos += len;
@@ -1188,14 +1265,14 @@ struct Enc {
 
 // LDS layout of one stream's workgroup; shared by the kernel (carving) and
 // the host (dynamic LDS size). Regions are 16-byte aligned.
-enum { L_PP, L_PROBS, L_LENP, L_LENC, L_PSP, L_DP, L_AP, L_TP, L_MDLEN, L_MDDIST, L_RINFO, L_RPAIRS, L_OPRICE,
-       L_OPP, L_OBP, L_OBP2, L_OFS, L_OBACKS, L_WIN, L_OBUF, L_LIT, L_COUNT };
+enum { L_PP, L_PROBS, L_DMP, L_LENP, L_LENC, L_PSP, L_DP, L_AP, L_TP, L_MDLEN, L_MDDIST, L_RINFO, L_RPAIRS, L_OPRICE,
+       L_OPP, L_OBP, L_OBP2, L_OFS, L_OBACKS, L_OBYTES, L_WIN, L_OBUF, L_LIT, L_COUNT };
 __host__ __device__ inline uint32_t enc_lds_layout(const EncArgs& a, uint32_t* off) {
     const uint32_t md_cap = a.fb + 2;   // pairs per position <= fb (+1 clamp slot)
     const uint32_t sz[L_COUNT] = {
-        512 * 2, prob_count(a.pb) * 2, 2 * (1u << a.pb) * a.len_table_size * 2, 2 * 16 * 4, 256 * 2, 512 * 2, 16 * 4,
-        kNumFullDistances * 2, md_cap * 2, md_cap * 4, kRing * 4, kRing * kInlinePairs * a.pair_bytes, kOptLds * 4, kOptLds * 4,
-        kOptLds * 4, kOptLds * 4, kOptLds, 4 * kOptLds * 4, kSides * kGW, kObuf,
+        512 * 2, prob_count(a.pb) * 2, dm_count(a.pb) * 4, 2 * (1u << a.pb) * a.len_table_size * 2, 2 * 16 * 4, 256 * 2, 512 * 2, 16 * 4,
+        0u /* tp aliases the gather window */, md_cap * 2, md_cap * 4, kRing * 4, kRing * kInlinePairs * a.pair_bytes, kOptLds * 4, kOptLds * 4,
+        kOptLds * 4, kOptLds * 4, kOptLds, 4 * kOptLds * 4, kOptLds * 4, kSides * kGW, kObuf,
         a.lit_in_lds ? (0x300u << (a.lc + a.lp)) * 2 : 0u};
     uint32_t o = 0;
     for (int i = 0; i < L_COUNT; i++) { if (off) off[i] = o; o += (sz[i] + 15) & ~15u; }
@@ -1229,7 +1306,8 @@ __global__ void __launch_bounds__(kWave, 4) enc_kernel(EncArgs a) {
     e.psp = (uint16_t*)(smem + off[L_PSP]);
     e.dp = (uint16_t*)(smem + off[L_DP]);
     e.ap = (uint32_t*)(smem + off[L_AP]);
-    e.tp = (uint16_t*)(smem + off[L_TP]);
+    e.tp = (uint16_t*)(smem + off[L_WIN]);   // tempPrices only live inside fill_distances_prices
+    e.dmp = (uint32_t*)(smem + off[L_DMP]);
     e.md_len = (uint16_t*)(smem + off[L_MDLEN]);
     e.md_dist = (uint32_t*)(smem + off[L_MDDIST]);
     e.ring_info = (uint32_t*)(smem + off[L_RINFO]);
@@ -1240,11 +1318,12 @@ __global__ void __launch_bounds__(kWave, 4) enc_kernel(EncArgs a) {
     e.o_bp2 = (int32_t*)(smem + off[L_OBP2]);
     e.o_fs = smem + off[L_OFS];
     e.o_backs = (uint32_t*)(smem + off[L_OBACKS]);
+    e.o_bytes = (uint32_t*)(smem + off[L_OBYTES]);
     e.win = smem + off[L_WIN];
     e.obuf = smem + off[L_OBUF];
     uint8_t* scratch = a.scratch + (size_t)blockIdx.x * a.scratch_stride;
-    e.spill = __builtin_amdgcn_make_buffer_rsrc(scratch, 0, kNumOpts * 4 * 9, 0x00020000);
-    uint16_t* lit_g = (uint16_t*)(scratch + kNumOpts * 4 * 9);
+    e.spill = __builtin_amdgcn_make_buffer_rsrc(scratch, 0, kNumOpts * 4 * 10, 0x00020000);
+    uint16_t* lit_g = (uint16_t*)(scratch + kNumOpts * 4 * 10);
     if (LIT_LDS) e.lit = (uint16_t*)(smem + off[L_LIT]);
     else e.lit = lit_g;
     for (int i0 = 0; i0 < 512; i0 += kWave) e.pp[i0 + e.lane] = (uint16_t)c_tab.prices[i0 + e.lane];
@@ -1292,7 +1371,7 @@ __global__ void __launch_bounds__(kWave, 4) enc_kernel(EncArgs a) {
 size_t enc_lds_bytes(const EncArgs& a) { return enc_lds_layout(a, nullptr); }
 
 size_t enc_scratch_per_block(const Derived& d) {
-    return (size_t)kNumOpts * 4 * 9 + ((size_t)0x300 << (d.lc + d.lp)) * 2 + 256;
+    return (size_t)kNumOpts * 4 * 10 + ((size_t)0x300 << (d.lc + d.lp)) * 2 + 256;
 }
 
 uint32_t enc_lit_in_lds(const Derived& d) { return (d.lc + d.lp) <= (uint32_t)kLitLdsMaxBits; }
