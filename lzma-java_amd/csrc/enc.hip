@@ -609,11 +609,19 @@ struct Enc {
         uint32_t slot = q - ring_base;
         uint32_t info = ring_info[slot];
         uint32_t cnt = info & 0xFFFFu, ml = info >> 16;
-        LANE_FOR(uint32_t, k, 0u, cnt) {
-            PairT pr = k < (uint32_t)kInlinePairs ? ring_pairs[slot * kInlinePairs + k]
-                                                  : ovf[ovf_off[gbase + q] + k - kInlinePairs];
-            md_len[k] = (uint16_t)PP::len(pr);
-            md_dist[k] = PP::dist(pr);
+        if (cnt <= (uint32_t)kInlinePairs) {   // LDS only (no wait on outstanding HBM operations)
+            LANE_FOR(uint32_t, k, 0u, cnt) {
+                const PairT pr = ring_pairs[slot * kInlinePairs + k];
+                md_len[k] = (uint16_t)PP::len(pr);
+                md_dist[k] = PP::dist(pr);
+            }
+        } else {
+            LANE_FOR(uint32_t, k, 0u, cnt) {
+                PairT pr = k < (uint32_t)kInlinePairs ? ring_pairs[slot * kInlinePairs + k]
+                                                      : ovf[ovf_off[gbase + q] + k - kInlinePairs];
+                md_len[k] = (uint16_t)PP::len(pr);
+                md_dist[k] = PP::dist(pr);
+            }
         }
         LANE_FENCE();
         num_pairs = cnt;
@@ -720,6 +728,23 @@ struct Enc {
         }
         fence_upto(base_slot + hi);
     }
+    // getOptimum's match candidates of position 0 (Encoder.java:620-640)
+    template <bool F>
+    FI void relax_first(uint32_t lstart, uint32_t len_main, uint32_t npairs, uint32_t normal_match_price, uint32_t pos_state) {
+        LANE_FOR(uint32_t, l, lstart, len_main + 1) {
+            uint32_t k = 0;
+            while (k + 1 < npairs && l > md_len[k]) k++;
+            uint32_t distance = md_dist[k];
+            uint32_t cl = normal_match_price + pos_len_price(distance, l, pos_state);
+            if (cl < price_at<F>(l)) {
+                set_price<F>(l, cl);
+                set_pp<F>(l, pp_at<F>(l) & 0xFFFF0000u);
+                set_bp<F>(l, (int32_t)(distance + kNumRepDistances));
+                set_fs<F>(l, fs_at<F>(l) & ~1u);
+            }
+        }
+        if (F) LANE_FENCE(); else fence_upto(len_main);
+    }
     // uniform single-slot update for the two-step (x + literal + rep0) candidates
     template <bool F> FI void relax_two_step_t(uint32_t s, uint32_t cl, uint32_t pos_prev_v, bool prev2, uint32_t pos_prev2_v, int32_t back2) {
         if (cl < price_at<F>(s)) {
@@ -802,7 +827,7 @@ struct Enc {
         PCOUNT(PF_NOPT);
         PBEGIN(t0);
         gather(false);
-        set_bytes(0, win_bytes());
+        set_bytes<true>(0, win_bytes());
         uint32_t num_avail = avail() + 1;
         if (num_avail < 2) { *back_res = -1; LANE_FENCE(); return 1; }
         if (num_avail > (uint32_t)kMatchMaxLen) num_avail = kMatchMaxLen;
@@ -829,7 +854,7 @@ struct Enc {
         uint32_t match_byte = b_byte(1, rp0, 0);   // rp0 == rd0 here
         if (len_main < 2 && cur_byte != match_byte && rl_max < 2) { *back_res = -1; return 1; }
 
-        set_fs(0, (fs_at(0) & 0xFu) | (state << 4));
+        set_fs<true>(0, (fs_at<true>(0) & 0xFu) | (state << 4));
         uint32_t pos_state = position & ps_mask;
         PBEGIN(t1);
         uint32_t p1 = dm0(E_IS_MATCH + (state << PBS) + pos_state) +
@@ -842,17 +867,22 @@ struct Enc {
             uint32_t srp = rep_match_price + rep_len1_price(state, pos_state);
             if (srp < p1) { p1 = srp; bp1 = 0; }
         }
-        set_price(1, p1);
-        set_bp(1, bp1);
-        set_fs(1, fs_at(1) & ~1u);
+        set_price<true>(1, p1);
+        set_bp<true>(1, bp1);
+        set_fs<true>(1, fs_at<true>(1) & ~1u);
         uint32_t len_end = len_main >= rl_max ? len_main : rl_max;
         if (len_end < 2) { *back_res = bp1; LANE_FENCE(); return 1; }
-        set_pp(1, pp_at(1) & 0xFFFF0000u);
-        set_back(0, 0, rp0); set_back(0, 1, rp1); set_back(0, 2, rp2); set_back(0, 3, rp3);
+        set_pp<true>(1, pp_at<true>(1) & 0xFFFF0000u);
+        set_back<true>(0, 0, rp0); set_back<true>(0, 1, rp1); set_back<true>(0, 2, rp2); set_back<true>(0, 3, rp3);
         LANE_FENCE();
         PBEGIN(t2);
-        LANE_FOR(uint32_t, l, 2u, len_end + 1) set_price(l, kInfinityPrice);
-        fence_upto(len_end);
+        if (len_end < (uint32_t)kOptLds) {
+            LANE_FOR(uint32_t, l, 2u, len_end + 1) set_price<true>(l, kInfinityPrice);
+            LANE_FENCE();
+        } else {
+            LANE_FOR(uint32_t, l, 2u, len_end + 1) set_price(l, kInfinityPrice);
+            fence_upto(len_end);
+        }
 #pragma unroll
         for (uint32_t i = 0; i < (uint32_t)kNumRepDistances; i++) {
             uint32_t rl = sel4(i, rl0, rl1, rl2, rl3);
@@ -863,19 +893,8 @@ struct Enc {
         uint32_t lstart = rl0 >= 2 ? rl0 + 1 : 2;
         if (lstart <= len_main) {
             // no look-ahead in this loop: every length is independent
-            LANE_FOR(uint32_t, l, lstart, len_main + 1) {
-                uint32_t k = 0;
-                while (k + 1 < npairs && l > md_len[k]) k++;
-                uint32_t distance = md_dist[k];
-                uint32_t cl = normal_match_price + pos_len_price(distance, l, pos_state);
-                if (cl < price_at(l)) {
-                    set_price(l, cl);
-                    set_pp(l, pp_at(l) & 0xFFFF0000u);
-                    set_bp(l, (int32_t)(distance + kNumRepDistances));
-                    set_fs(l, fs_at(l) & ~1u);
-                }
-            }
-            fence_upto(len_main);
+            if (len_main < (uint32_t)kOptLds) relax_first<true>(lstart, len_main, npairs, normal_match_price, pos_state);
+            else relax_first<false>(lstart, len_main, npairs, normal_match_price, pos_state);
         }
         PEND(PF_RELAX, t2);
         return parse_forward(position, back_res, len_end);
