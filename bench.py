@@ -144,8 +144,9 @@ def main():
     else:
         alg = (size + comp_bytes) / per_step_launches    # N_in + N_out per launch
     achieved = alg / avg_s if avg_s > 0 else 0.0
+    traffic, traffic_src = pmc_traffic(dname, args.size, args.chunk)
     roofline = {"bound": "hbm", "kernel": dname, "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
-                "unit": "GB/s", "frac": achieved / HBM_PEAK, "traffic": None,
+                "unit": "GB/s", "frac": achieved / HBM_PEAK, "traffic": traffic, "traffic_source": traffic_src,
                 "avg_launch_ms": avg_s * 1e3, "launches_per_step": per_step_launches,
                 "alg_bytes_per_launch": alg}
 
@@ -177,6 +178,30 @@ def main():
         torch.distributed.destroy_process_group()
     if not ok:
         sys.exit(1)
+
+
+# HIP-event timing label -> rocprofv3 kernel-name prefix
+_KERNEL_OF = {"enc_parse": "enc_kernel", "dec_stream": "dec_kernel", "mf_walk": "mf_walk_kernel"}
+
+
+def pmc_traffic(label, size, chunk):
+    """HBM bytes per launch of the dominant kernel from the committed PMC
+    summary (profiles/traffic.json, written by tools/profile_round.sh from
+    separate FETCH_SIZE / WRITE_SIZE passes over this same workload), or None
+    when that summary is absent or was taken on another workload."""
+    path = os.path.join(REPO, "profiles", "traffic.json")
+    if not os.path.exists(path):
+        return None, None
+    with open(path) as f:
+        t = json.load(f)
+    meta = t.get("_workload", {})
+    if meta.get("bytes_per_gpu") != size or meta.get("chunk") != chunk:
+        return None, None
+    prefix = _KERNEL_OF.get(label, label)
+    for k, v in t.items():
+        if k.startswith(prefix) and isinstance(v, dict) and "traffic_bytes_per_launch" in v:
+            return v["traffic_bytes_per_launch"], "profiles/traffic.json (%s, rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)" % k
+    return None, None
 
 
 def cpu_baseline(host, chunk, sample, p, threads):

@@ -75,7 +75,7 @@ struct Dec {
         for (uint32_t k0 = 0; k0 < kIbuf; k0 += kWave) {   // uniform trip count
             const uint32_t k = k0 + lane;
             const uint32_t q = base + k;
-            ibuf[k] = q < n_in ? in[q] : 0;
+            ibuf[k] = q < n_in ? __builtin_nontemporal_load(in + q) : 0;   // streamed once
         }
         LANE_FENCE();
     }
@@ -91,7 +91,7 @@ struct Dec {
         LANE_FENCE();
         for (uint32_t k0 = flushed; k0 < upto; k0 += kWave) {   // uniform trip count
             const uint32_t k = k0 + lane;
-            if (k < upto) out[k] = win[k & (kWin - 1)];
+            if (k < upto) __builtin_nontemporal_store(win[k & (kWin - 1)], out + k);
         }
         flushed = upto;
         LANE_FENCE();

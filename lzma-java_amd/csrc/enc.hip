@@ -382,7 +382,7 @@ struct Enc {
     FI void flush_out(uint32_t start, uint32_t count) {
         LANE_FENCE();
         LANE_FOR(uint32_t, i, 0u, count)
-            if (start + i < cap) out[start + i] = obuf[i];
+            if (start + i < cap) __builtin_nontemporal_store(obuf[i], out + start + i);
         LANE_FENCE();
     }
     FI void put_byte(uint32_t b) {
@@ -592,9 +592,11 @@ struct Enc {
             PairT p0 = 0, p1 = 0, p2 = 0, p3 = 0;
             if (q < n) {
                 uint64_t g0 = gbase + q;
-                info = minfo[g0];
+                // streamed once: non-temporal, so they do not evict the literal models from L2
+                info = __builtin_nontemporal_load(minfo + g0);
                 const PairT* src = pairs + g0 * kInlinePairs;
-                p0 = src[0]; p1 = src[1]; p2 = src[2]; p3 = src[3];
+                p0 = __builtin_nontemporal_load(src + 0); p1 = __builtin_nontemporal_load(src + 1);
+                p2 = __builtin_nontemporal_load(src + 2); p3 = __builtin_nontemporal_load(src + 3);
             }
             ring_info[k] = info;
             PairT* dst = ring_pairs + k * kInlinePairs;

@@ -13,7 +13,7 @@
 //   K3 mf_links    prev-in-bucket for hash2/hash3; bucket (chain) heads
 //   K4 mf_walk     one lane per bucket: replays BinTree.fillMatches0
 //                  (:152-273) for the bucket's positions in order, with the
-//                  son[] links indexed by absolute position (window expiry
+//                  son[] links indexed by sorted bucket index (window expiry
 //                  via matchMinPos makes cyclic reuse unobservable).
 // Output per position: minfo = count | main_len << 16 (main_len = longest
 // pair extended past fb as Encoder.ReadMatchDistances does, Encoder.java:
@@ -92,12 +92,20 @@ __global__ void __launch_bounds__(256) mf_heads_kernel(const uint64_t* __restric
     }
 }
 
+// chain lengths, and the walk-order key (stream ascending, length descending):
+// the walk then works through the streams in order, so the lanes resident at
+// one time read a few streams' bytes (cache-resident) instead of the whole batch
 __global__ void __launch_bounds__(256) mf_chain_len_kernel(const uint32_t* __restrict__ starts, const uint64_t* __restrict__ nchains_p,
-                                                           const uint64_t* __restrict__ nvalid_p, uint32_t* __restrict__ lens) {
+                                                           const uint64_t* __restrict__ nvalid_p, const uint64_t* __restrict__ keys,
+                                                           uint32_t key_shift, uint32_t* __restrict__ lens,
+                                                           uint32_t* __restrict__ order_key) {
     uint64_t nchains = *nchains_p, nvalid = *nvalid_p;
     for (uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; c < nchains; c += (uint64_t)gridDim.x * blockDim.x) {
         uint64_t e = (c + 1 < nchains) ? starts[c + 1] : nvalid;
-        lens[c] = (uint32_t)(e - starts[c]);
+        const uint32_t len = (uint32_t)(e - starts[c]);
+        lens[c] = len;
+        const uint32_t stream = (uint32_t)(keys[starts[c]] >> key_shift);   // < 2^14 streams per pass
+        order_key[c] = (stream << 18) | (0x3FFFFu - (len < 0x3FFFFu ? len : 0x3FFFFu));
     }
 }
 
@@ -137,7 +145,11 @@ __global__ void __launch_bounds__(64) mf_walk_kernel(const uint8_t* __restrict__
                                                      int* __restrict__ err) {
     using PP = PairPack<PairT>;
     uint64_t nchains = *nchains_p;
-    uint64_t ci = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    // XCD-aware mapping: the dispatcher places block b on XCD b % 8, so XCD x takes
+    // the x-th eighth of the (stream-ordered) chain list and its L2 serves a few streams
+    const uint32_t per_xcd = gridDim.x / 8;   // the host pads the grid to a multiple of 8
+    const uint64_t blk = (uint64_t)(blockIdx.x % 8) * per_xcd + blockIdx.x / 8;
+    uint64_t ci = blk * blockDim.x + threadIdx.x;
     if (ci >= nchains) return;
     uint32_t c = chain_order[ci];
     uint64_t start = chain_start[c], end = start + chain_len[c];
@@ -148,6 +160,10 @@ __global__ void __launch_bounds__(64) mf_walk_kernel(const uint8_t* __restrict__
     const uint32_t fb = a.fb, cut = a.cut_value;
     const uint64_t cyc = a.cyc_size;
     uint32_t prev_local = 0;                // 1-based local position of previous bucket member, 0 = none
+    // son[] is indexed by the member's index in the sorted key array (not by
+    // position): a bucket's tree links then live in one contiguous run
+    // [2 start, 2 end), so a walk touches a few cache lines instead of one
+    // random line per step. Links hold sorted index + 1 (0 = no node).
     for (uint64_t i = start; i < end; i++) {
         uint64_t g = vals4[i];
         uint32_t p = (uint32_t)(g - base);
@@ -187,7 +203,8 @@ __global__ void __launch_bounds__(64) mf_walk_kernel(const uint8_t* __restrict__
             }
             if (cnt != 0 && cm2 == cur_match) { cnt--; max_len = 1; }
         }
-        uint64_t ptr0 = 2 * g + 1, ptr1 = 2 * g;
+        uint64_t ptr0 = 2 * i + 1, ptr1 = 2 * i;
+        uint64_t cur_idx = i - 1;           // sorted index of the head (valid while cur_match != 0)
         uint32_t len0 = a.direct_bytes, len1 = a.direct_bytes;
         if (!BT4 && cur_match > match_min) {   // BT2 direct byte check, BinTree.java:218-226
             if (sb[cur_match - 1 + 2] != cur[2]) { max_len = 2; emit(2, pos - cur_match - 1); }
@@ -196,7 +213,7 @@ __global__ void __launch_bounds__(64) mf_walk_kernel(const uint8_t* __restrict__
         for (;;) {   // BinTree.java:230-270
             if (cur_match <= match_min || count-- == 0) { son[ptr0] = 0; son[ptr1] = 0; break; }
             uint32_t delta = pos - cur_match;
-            uint64_t cp = 2 * (base + cur_match - 1);
+            uint64_t cp = 2 * cur_idx;
             const uint8_t* pby = sb + (cur_match - 1);
             uint32_t len = len0 < len1 ? len0 : len1;
             if (pby[len] == cur[len]) {
@@ -207,8 +224,11 @@ __global__ void __launch_bounds__(64) mf_walk_kernel(const uint8_t* __restrict__
                     if (len == len_limit) { son[ptr1] = son[cp]; son[ptr0] = son[cp + 1]; break; }
                 }
             }
-            if (pby[len] < cur[len]) { son[ptr1] = cur_match; ptr1 = cp + 1; cur_match = son[ptr1]; len1 = len; }
-            else { son[ptr0] = cur_match; ptr0 = cp; cur_match = son[ptr0]; len0 = len; }
+            uint32_t nxt;
+            if (pby[len] < cur[len]) { son[ptr1] = (uint32_t)(cur_idx + 1); ptr1 = cp + 1; nxt = son[ptr1]; len1 = len; }
+            else { son[ptr0] = (uint32_t)(cur_idx + 1); ptr0 = cp; nxt = son[ptr0]; len0 = len; }
+            if (nxt == 0) cur_match = 0;
+            else { cur_idx = nxt - 1; cur_match = (uint32_t)(vals4[cur_idx] - base) + 1; }
         }
         uint32_t ml = 0;
         if (cnt > 0) {   // Encoder.ReadMatchDistances extension, Encoder.java:279-284
@@ -309,12 +329,17 @@ int run_match_finder(Ctx* ctx, const Derived& d, const uint8_t* in, const uint64
     if (hipStreamSynchronize(st) != hipSuccess) return ctx->fail(LZMA_E_DEVICE, "sync after chain select");
     uint64_t nchains = hc[1];
     if (nchains == 0) return LZMA_OK;
-    hipLaunchKernelGGL(mf_chain_len_kernel, dim3(grid_for(nchains, B)), dim3(B), 0, st, w.chain_start, w.counts + 1, w.counts, w.chain_len);
-    // longest chains first so lanes of one wave walk similar-length buckets
+    // walk order: stream by stream (cache locality), longest chains first within a
+    // stream (lanes of one wave walk similar-length buckets). The k2/k3 key arrays are
+    // dead here and hold the order keys.
+    uint32_t* okey = (uint32_t*)w.k2;
+    uint32_t* okey_sorted = (uint32_t*)w.k3;
+    hipLaunchKernelGGL(mf_chain_len_kernel, dim3(grid_for(nchains, B)), dim3(B), 0, st, w.chain_start, w.counts + 1, w.counts,
+                       w.ks, bt4 ? d.hash_bits : 16u, w.chain_len, okey);
     {
         TimedLaunch tl(ctx, "mf_sort", st);
         hipLaunchKernelGGL(iota_kernel, dim3(grid_for(nchains, B)), dim3(B), 0, st, w.chain_idx, nchains);
-        if ((rc = radix_sort(ctx, w.chain_len, w.chain_len_sorted, w.chain_idx, w.chain_order, nchains, 32, st, true))) return rc;
+        if ((rc = radix_sort(ctx, okey, okey_sorted, w.chain_idx, w.chain_order, nchains, 32, st))) return rc;
     }
     hipMemsetAsync(w.ovf_used, 0, sizeof(unsigned long long), st);
     hipMemsetAsync(w.err, 0, sizeof(int), st);
@@ -322,6 +347,7 @@ int run_match_finder(Ctx* ctx, const Derived& d, const uint8_t* in, const uint64
         TimedLaunch tl(ctx, "mf_walk", st);
         const unsigned WB = 64;
         unsigned grid = (unsigned)((nchains + WB - 1) / WB);
+        grid = (grid + 7) & ~7u;   // multiple of 8 (XCD-aware mapping in mf_walk_kernel)
         if (wide_pairs) {
             if (bt4) hipLaunchKernelGGL((mf_walk_kernel<uint64_t, true>), dim3(grid), dim3(WB), 0, st, in, d_offs, w.ks, w.vs, w.chain_order, w.chain_start, w.chain_len, w.counts + 1, a, w.son, (uint64_t*)w.pairs, w.ovf_off, (uint64_t*)w.ovf, w.ovf_used, w.ovf_cap, w.err);
             else hipLaunchKernelGGL((mf_walk_kernel<uint64_t, false>), dim3(grid), dim3(WB), 0, st, in, d_offs, w.ks, w.vs, w.chain_order, w.chain_start, w.chain_len, w.counts + 1, a, w.son, (uint64_t*)w.pairs, w.ovf_off, (uint64_t*)w.ovf, w.ovf_used, w.ovf_cap, w.err);
