@@ -28,6 +28,7 @@ namespace lzg {
 static __constant__ Tables c_tab = make_tables();
 
 constexpr uint64_t kSentinel = ~0ull;
+constexpr uint32_t kSentinel32 = ~0u;
 
 __device__ inline int find_stream(const uint64_t* offs, int nstreams, uint64_t g) {
     // largest s with offs[s] <= g (offs has nstreams+1 entries, offs[nstreams] = total)
@@ -51,7 +52,7 @@ __global__ void __launch_bounds__(256) mf_keys_kernel(const uint8_t* __restrict_
         uint32_t len_limit = rem < a.fb ? (uint32_t)rem : a.fb;
         if (len_limit < a.min_match_check) {   // BinTree.java:153-162: no insertion
             a.k4[g] = kSentinel;
-            if (BT4) { a.k3[g] = kSentinel; a.k2[g] = kSentinel; }
+            if (BT4) { a.k3[g] = kSentinel32; a.k2[g] = kSentinel32; }
             continue;
         }
         uint32_t b0 = in[g], b1 = in[g + 1];
@@ -63,8 +64,8 @@ __global__ void __launch_bounds__(256) mf_keys_kernel(const uint8_t* __restrict_
             uint32_t h3 = temp & 0xFFFFu;
             uint32_t hv = (temp ^ (c_tab.crc[b3] << 5)) & a.hash_mask;
             a.k4[g] = ((uint64_t)s << a.hash_bits) | hv;
-            a.k3[g] = ((uint64_t)s << 16) | h3;
-            a.k2[g] = ((uint64_t)s << 10) | h2;
+            a.k3[g] = ((uint32_t)s << 16) | h3;
+            a.k2[g] = ((uint32_t)s << 10) | h2;
         } else {
             a.k4[g] = ((uint64_t)s << 16) | (b0 ^ (b1 << 8));
         }
@@ -72,11 +73,11 @@ __global__ void __launch_bounds__(256) mf_keys_kernel(const uint8_t* __restrict_
 }
 
 // prev-in-bucket for a position-ordered sorted key array (hash2 / hash3 heads)
-__global__ void __launch_bounds__(256) mf_prev_kernel(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ vals,
+__global__ void __launch_bounds__(256) mf_prev_kernel(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ vals,
                                                       uint64_t total, uint32_t* __restrict__ prev) {
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < total; i += (uint64_t)gridDim.x * blockDim.x) {
-        uint64_t k = keys[i];
-        if (k == kSentinel) continue;
+        uint32_t k = keys[i];
+        if (k == kSentinel32) continue;
         prev[vals[i]] = (i > 0 && keys[i - 1] == k) ? vals[i - 1] : kNoPos;
     }
 }
@@ -286,7 +287,7 @@ int run_match_finder(Ctx* ctx, const Derived& d, const uint8_t* in, const uint64
     MfArgs a{};
     a.fb = d.fb; a.min_match_check = d.min_match_check; a.hash_mask = d.hash_mask; a.hash_bits = d.hash_bits;
     a.cut_value = d.cut_value; a.cyc_size = d.cyc_size; a.direct_bytes = d.direct_bytes;
-    a.k4 = w.k4; a.k3 = w.k3; a.k2 = w.k2; a.vals = w.vals; a.minfo = w.minfo; a.prev2 = w.prev2; a.prev3 = w.prev3;
+    a.k4 = w.k4; a.k3 = (uint32_t*)w.k3; a.k2 = (uint32_t*)w.k2; a.vals = w.vals; a.minfo = w.minfo; a.prev2 = w.prev2; a.prev3 = w.prev3;
     const bool bt4 = d.hash_array != 0;
     const unsigned B = 256;
     const uint32_t sbits = bits_for((uint64_t)nstreams) + 1;
@@ -300,14 +301,14 @@ int run_match_finder(Ctx* ctx, const Derived& d, const uint8_t* in, const uint64
     if (bt4) {
         {
             TimedLaunch tl(ctx, "mf_sort", st);
-            if ((rc = radix_sort(ctx, w.k2, w.ks, w.vals, w.vs, total, (int)(10 + sbits), st))) return rc;
+            if ((rc = radix_sort(ctx, (uint32_t*)w.k2, (uint32_t*)w.ks, w.vals, w.vs, total, (int)(10 + sbits), st))) return rc;
         }
-        hipLaunchKernelGGL(mf_prev_kernel, dim3(grid_for(total, B)), dim3(B), 0, st, w.ks, w.vs, total, w.prev2);
+        hipLaunchKernelGGL(mf_prev_kernel, dim3(grid_for(total, B)), dim3(B), 0, st, (const uint32_t*)w.ks, w.vs, total, w.prev2);
         {
             TimedLaunch tl(ctx, "mf_sort", st);
-            if ((rc = radix_sort(ctx, w.k3, w.ks, w.vals, w.vs, total, (int)(16 + sbits), st))) return rc;
+            if ((rc = radix_sort(ctx, (uint32_t*)w.k3, (uint32_t*)w.ks, w.vals, w.vs, total, (int)(16 + sbits), st))) return rc;
         }
-        hipLaunchKernelGGL(mf_prev_kernel, dim3(grid_for(total, B)), dim3(B), 0, st, w.ks, w.vs, total, w.prev3);
+        hipLaunchKernelGGL(mf_prev_kernel, dim3(grid_for(total, B)), dim3(B), 0, st, (const uint32_t*)w.ks, w.vs, total, w.prev3);
     }
     {
         TimedLaunch tl(ctx, "mf_sort", st);

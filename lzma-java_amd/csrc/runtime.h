@@ -24,7 +24,8 @@ namespace lzg {
 struct MfArgs {
     uint32_t fb, min_match_check, hash_mask, hash_bits, cut_value, direct_bytes;
     uint64_t cyc_size;
-    uint64_t *k4, *k3, *k2;
+    uint64_t* k4;
+    uint32_t *k3, *k2;            // (stream << 16 | hash3), (stream << 10 | hash2): < 2^30 for <= 16384 streams
     uint32_t *vals, *minfo, *prev2, *prev3;
 };
 
