@@ -283,12 +283,18 @@ struct Dec {
                 // LiteralDecoder.Decoder2.DecodeNormal / DecodeWithMatchByte (Decoder.java:67-102)
                 uint32_t sym = 1;
                 bool same = matched;
-#pragma unroll 1
+                // unrolled: level i's nodes are [2^i, 2^(i+1)), so levels 0-6 read the
+                // low lane vector only (a static choice)
+#pragma unroll
                 for (uint32_t i = 0; i < 8; i++) {
                     uint32_t np, idx, prob;
                     const uint32_t mbit = (mb >> (7 - i)) & 1u;
                     if (same) { idx = ((1 + mbit) << 8) + sym; prob = vget(mv, i); }
-                    else { idx = sym; prob = node256(tlo, thi, sym); }
+                    else {
+                        idx = sym;
+                        if (i < 7) prob = (vget(tlo, sym >> 1) >> ((sym & 1u) << 4)) & 0xFFFFu;
+                        else prob = node256(tlo, thi, sym);
+                    }
                     const uint32_t x = dbit(prob, &np);
                     sub[idx] = (uint16_t)np;   // every lane, same address and value
                     if (same && x != mbit) same = false;
