@@ -215,13 +215,23 @@ struct Dec {
             else { base = PL::HIGH; off = 0; nb = 8; sym0 = kNumLowLenSymbols + kNumMidLenSymbols; }
         }
         uint32_t m = 1;
-        for (uint32_t b = nb; b != 0; b--) {
-            const uint32_t prob = nb == 3 ? vget(lv, off + m) : node256(lo, hi, m);
+        if (nb == 3) {   // unrolled walks: static trip counts and lane-vector choices
+#pragma unroll
+            for (int b = 0; b < 3; b++) {
+                x = dbit(vget(lv, off + m), &np);
+                L[base + m] = (uint16_t)np;
+                m = (m << 1) + x;
+            }
+            return sym0 + m - 8u;
+        }
+#pragma unroll
+        for (int b = 0; b < 8; b++) {
+            const uint32_t prob = b < 7 ? (vget(lo, m >> 1) >> ((m & 1u) << 4)) & 0xFFFFu : node256(lo, hi, m);
             x = dbit(prob, &np);
             L[base + m] = (uint16_t)np;
             m = (m << 1) + x;
         }
-        return sym0 + m - (1u << nb);
+        return sym0 + m - 256u;
     }
     // OutWindow.CopyBlock (OutWindow.java:53-67) of len bytes at distance d1,
     // byte-serial semantics: an overlapping copy repeats the d1-byte period.
