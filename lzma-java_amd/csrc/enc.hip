@@ -1344,7 +1344,7 @@ __global__ void __launch_bounds__(kWave, 4) enc_kernel(EncArgs a) {
     e.obuf = smem + off[L_OBUF];
     uint8_t* scratch = a.scratch + (size_t)blockIdx.x * a.scratch_stride;
     e.spill = __builtin_amdgcn_make_buffer_rsrc(scratch, 0, kNumOpts * 4 * 10, 0x00020000);
-    uint16_t* lit_g = (uint16_t*)(scratch + kNumOpts * 4 * 10);
+    uint16_t* lit_g = (uint16_t*)(a.lit_scratch + (size_t)blockIdx.x * a.lit_stride);
     if (LIT_LDS) e.lit = (uint16_t*)(smem + off[L_LIT]);
     else e.lit = lit_g;
     for (int i0 = 0; i0 < 512; i0 += kWave) e.pp[i0 + e.lane] = (uint16_t)c_tab.prices[i0 + e.lane];
@@ -1391,9 +1391,9 @@ __global__ void __launch_bounds__(kWave, 4) enc_kernel(EncArgs a) {
 
 size_t enc_lds_bytes(const EncArgs& a) { return enc_lds_layout(a, nullptr); }
 
-size_t enc_scratch_per_block(const Derived& d) {
-    return (size_t)kNumOpts * 4 * 10 + ((size_t)0x300 << (d.lc + d.lp)) * 2 + 256;
-}
+size_t enc_scratch_per_block(const Derived&) { return (size_t)kNumOpts * 4 * 10 + 256; }
+
+size_t enc_lit_bytes(const Derived& d) { return ((size_t)0x300 << (d.lc + d.lp)) * 2; }
 
 uint32_t enc_lit_in_lds(const Derived& d) { return (d.lc + d.lp) <= (uint32_t)kLitLdsMaxBits; }
 

@@ -94,6 +94,20 @@ struct Ctx {
         }
         return tmp;
     }
+    // literal-coder tables of the encoder and decoder: their own allocation, so the
+    // per-stream tables sit in one compact region (few TLB pages) instead of at a
+    // large stride inside the match-finder arena
+    uint8_t* litbuf = nullptr;
+    size_t litbuf_size = 0;
+    bool ensure_litbuf(size_t n) {
+        if (n <= litbuf_size) return true;
+        if (litbuf) hipFree(litbuf);
+        litbuf = nullptr;
+        litbuf_size = 0;
+        if (hipMalloc(&litbuf, n) != hipSuccess) return false;
+        litbuf_size = n;
+        return true;
+    }
     bool ensure_arena(size_t n) {
         if (n <= arena_size) return true;
         if (arena) hipFree(arena);
@@ -210,8 +224,10 @@ struct EncArgs {
     const uint64_t* out_offs;     // capacity layout (nstreams+1)
     uint64_t* out_lens;
     int32_t* status;
-    uint8_t* scratch;             // per-block global scratch
+    uint8_t* scratch;             // per-block global scratch (_optimum spill)
     uint64_t scratch_stride;
+    uint8_t* lit_scratch;         // per-block literal coders (when not in LDS), Ctx::litbuf
+    uint64_t lit_stride;
     uint32_t fb, lc, lp, pb, eos, dist_table_size, len_table_size;
     uint32_t lit_in_lds;
     uint32_t pair_bytes;          // 4 (u32 packed pairs) or 8 (u64, streams >= 8 MiB)
@@ -226,6 +242,7 @@ enum { PF_TOTAL, PF_GETOPT, PF_MATCHES, PF_REPLEN, PF_TWOLEN, PF_LIT, PF_RELAX, 
 int launch_encoder(Ctx* ctx, const EncArgs& a, bool wide_pairs, int grid, hipStream_t st);
 uint32_t enc_lit_in_lds(const Derived& d);
 size_t enc_scratch_per_block(const Derived& d);
+size_t enc_lit_bytes(const Derived& d);
 
 struct DecArgs {
     const uint8_t* in;

@@ -155,6 +155,9 @@ static int encode_pass(Ctx* ctx, const Derived& d, const uint8_t* d_in, const ui
         a.minfo = w.minfo; a.pairs = w.pairs; a.ovf_off = w.ovf_off; a.ovf = w.ovf;
         a.out = d_out; a.out_offs = d_oofs; a.out_lens = d_lens; a.status = d_status;
         a.scratch = d_scr; a.scratch_stride = scr;
+        a.lit_stride = (enc_lit_bytes(d) + 255) & ~(size_t)255;
+        if (!ctx->ensure_litbuf((size_t)grid * a.lit_stride + 256)) return ctx->fail(LZMA_E_NOMEM, "literal-coder tables");
+        a.lit_scratch = ctx->litbuf;
         a.fb = d.fb; a.lc = d.lc; a.lp = d.lp; a.pb = d.pb; a.eos = d.eos;
         a.dist_table_size = d.dist_table_size; a.len_table_size = d.len_table_size;
         a.lit_in_lds = enc_lit_in_lds(d);
@@ -237,7 +240,7 @@ static int decode_batch_dev(Ctx* ctx, const uint8_t props[5], const uint8_t* d_i
     Carver probe(nullptr);
     probe.take<uint64_t>(nstreams + 1); probe.take<int64_t>(nstreams); probe.take<uint64_t>(nstreams + 1);
     probe.take<uint64_t>(nstreams); probe.take<int32_t>(nstreams); probe.take<uint32_t>(nstreams);
-    probe.take<unsigned>(4); probe.take<uint8_t>((size_t)grid * scr + 16);
+    probe.take<unsigned>(4);
     if (!ctx->ensure_arena(probe.off + 4096)) return ctx->fail(LZMA_E_NOMEM, "decoder workspace");
     Carver c(ctx->arena);
     uint64_t* d_in_offs = c.take<uint64_t>(nstreams + 1);
@@ -247,7 +250,8 @@ static int decode_batch_dev(Ctx* ctx, const uint8_t props[5], const uint8_t* d_i
     int32_t* d_status = c.take<int32_t>(nstreams);
     uint32_t* d_order = c.take<uint32_t>(nstreams);
     unsigned* d_next = c.take<unsigned>(4);
-    uint8_t* d_scr = c.take<uint8_t>((size_t)grid * scr + 16);
+    if (!ctx->ensure_litbuf((size_t)grid * scr + 16)) return ctx->fail(LZMA_E_NOMEM, "decoder literal-coder tables");
+    uint8_t* d_scr = ctx->litbuf;
     HIPCHK(hipMemcpyAsync(d_in_offs, h_in_offs, (nstreams + 1) * 8, hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(d_sizes, h_out_sizes, nstreams * 8, hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(d_oofs, h_out_offs, (nstreams + 1) * 8, hipMemcpyHostToDevice, st));
@@ -332,6 +336,7 @@ void lzma_ctx_destroy(lzma_ctx* ctx) {
     ctx->resolve_timings();
     for (auto e : ctx->free_events) hipEventDestroy(e);
     if (ctx->arena) hipFree(ctx->arena);
+    if (ctx->litbuf) hipFree(ctx->litbuf);
     if (ctx->tmp) hipFree(ctx->tmp);
     delete ctx;
 }
