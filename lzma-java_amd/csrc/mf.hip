@@ -179,7 +179,9 @@ __global__ void __launch_bounds__(64) mf_walk_kernel(const uint8_t* __restrict__
         PairT* ov = nullptr;
         auto emit = [&](uint32_t l, uint32_t d) {
             if (cnt < kInlinePairs) {
-                inl[cnt] = PP::pack(l, d);
+                // outputs and the hash2/3 links are touched once: non-temporal, so the
+                // stream's tree links and bytes keep the L2
+                __builtin_nontemporal_store(PP::pack(l, d), inl + cnt);
             } else {
                 if (ov == nullptr) {
                     unsigned long long o = atomicAdd(ovf_used, (unsigned long long)(fb + 2));
@@ -192,7 +194,7 @@ __global__ void __launch_bounds__(64) mf_walk_kernel(const uint8_t* __restrict__
             cnt++;
         };
         if (BT4) {   // hash2 / hash3 candidates, BinTree.java:183-207
-            uint32_t pv2 = a.prev2[g], pv3 = a.prev3[g];
+            uint32_t pv2 = __builtin_nontemporal_load(a.prev2 + g), pv3 = __builtin_nontemporal_load(a.prev3 + g);
             uint32_t cm2 = pv2 == kNoPos ? 0 : (uint32_t)(pv2 - base) + 1;
             uint32_t cm3 = pv3 == kNoPos ? 0 : (uint32_t)(pv3 - base) + 1;
             if (cm2 > match_min && sb[cm2 - 1] == cur[0]) { max_len = 2; emit(2, pos - cm2 - 1); }
@@ -243,7 +245,7 @@ __global__ void __launch_bounds__(64) mf_walk_kernel(const uint8_t* __restrict__
                 ml += common_len(sb + from - d1, sb + from, 0, (uint32_t)lim);
             }
         }
-        a.minfo[g] = cnt | (ml << 16);
+        __builtin_nontemporal_store(cnt | (ml << 16), a.minfo + g);
         prev_local = pos;
     }
 }
