@@ -82,14 +82,14 @@ __global__ void __launch_bounds__(256) mf_prev_kernel(const uint32_t* __restrict
     }
 }
 
-// chain heads of the hash4 sort + number of valid (non-sentinel) entries
+// chain heads of the hash4 sort. The sorts are segmented per stream, so each
+// stream's non-inserted tail (sentinel keys) ends its own segment; a sentinel run
+// is a chain of its own that mf_chain_len_kernel empties.
 __global__ void __launch_bounds__(256) mf_heads_kernel(const uint64_t* __restrict__ keys, uint64_t total,
                                                        uint8_t* __restrict__ flag, uint64_t* __restrict__ nvalid) {
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < total; i += (uint64_t)gridDim.x * blockDim.x) {
-        uint64_t k = keys[i];
-        bool valid = k != kSentinel;
-        flag[i] = valid && (i == 0 || keys[i - 1] != k);
-        if (valid && (i + 1 == total || keys[i + 1] == kSentinel)) *nvalid = i + 1;
+        flag[i] = i == 0 || keys[i - 1] != keys[i];
+        if (i + 1 == total) *nvalid = total;
     }
 }
 
@@ -103,9 +103,15 @@ __global__ void __launch_bounds__(256) mf_chain_len_kernel(const uint32_t* __res
     uint64_t nchains = *nchains_p, nvalid = *nvalid_p;
     for (uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; c < nchains; c += (uint64_t)gridDim.x * blockDim.x) {
         uint64_t e = (c + 1 < nchains) ? starts[c + 1] : nvalid;
+        const uint64_t k = keys[starts[c]];
+        if (k == kSentinel) {   // positions with no insertion: nothing to walk, ordered last
+            lens[c] = 0;
+            order_key[c] = ~0u;
+            continue;
+        }
         const uint32_t len = (uint32_t)(e - starts[c]);
         lens[c] = len;
-        const uint32_t stream = (uint32_t)(keys[starts[c]] >> key_shift);   // < 2^14 streams per pass
+        const uint32_t stream = (uint32_t)(k >> key_shift);   // < 2^14 streams per pass
         order_key[c] = (stream << 18) | (0x3FFFFu - (len < 0x3FFFFu ? len : 0x3FFFFu));
     }
 }
@@ -154,6 +160,7 @@ __global__ void __launch_bounds__(64) mf_walk_kernel(const uint8_t* __restrict__
     if (ci >= nchains) return;
     uint32_t c = chain_order[ci];
     uint64_t start = chain_start[c], end = start + chain_len[c];
+    if (start == end) return;   // a stream's sentinel run
     uint64_t key = keys4[start];
     int s = (int)(key >> (BT4 ? a.hash_bits : 16));
     uint64_t base = offs[s], n = offs[s + 1] - base;
@@ -274,6 +281,23 @@ static int radix_sort(Ctx* ctx, const KeyT* kin, KeyT* kout, const ValT* vin, Va
     return LZMA_OK;
 }
 
+// Stable sort of each stream's positions by the low `end_bit` key bits: the
+// positions are stream-major already, so the stream bits need no digit passes.
+template <typename KeyT, typename ValT>
+static int segmented_sort(Ctx* ctx, const KeyT* kin, KeyT* kout, const ValT* vin, ValT* vout, uint64_t n,
+                          const uint64_t* d_offs, int nstreams, int end_bit, hipStream_t st) {
+    size_t tmp = 0;
+    hipError_t e = hipcub::DeviceSegmentedRadixSort::SortPairs(nullptr, tmp, kin, kout, vin, vout, (int)n, nstreams, d_offs,
+                                                              d_offs + 1, 0, end_bit, st);
+    if (e != hipSuccess) return ctx->fail(LZMA_E_DEVICE, "segmented sort sizing: %s", hipGetErrorString(e));
+    void* t = ctx->scratch(tmp);
+    if (!t && tmp) return ctx->fail(LZMA_E_NOMEM, "segmented sort temp %zu", tmp);
+    e = hipcub::DeviceSegmentedRadixSort::SortPairs(t, tmp, kin, kout, vin, vout, (int)n, nstreams, d_offs, d_offs + 1, 0,
+                                                   end_bit, st);
+    if (e != hipSuccess) return ctx->fail(LZMA_E_DEVICE, "segmented sort: %s", hipGetErrorString(e));
+    return LZMA_OK;
+}
+
 static inline unsigned grid_for(uint64_t n, unsigned block, unsigned cap = 65536) {
     uint64_t g = (n + block - 1) / block;
     if (g < 1) g = 1;
@@ -292,7 +316,6 @@ int run_match_finder(Ctx* ctx, const Derived& d, const uint8_t* in, const uint64
     a.k4 = w.k4; a.k3 = (uint32_t*)w.k3; a.k2 = (uint32_t*)w.k2; a.vals = w.vals; a.minfo = w.minfo; a.prev2 = w.prev2; a.prev3 = w.prev3;
     const bool bt4 = d.hash_array != 0;
     const unsigned B = 256;
-    const uint32_t sbits = bits_for((uint64_t)nstreams) + 1;
     {
         TimedLaunch tl(ctx, "mf_keys", st);
         if (bt4) hipLaunchKernelGGL((mf_keys_kernel<true>), dim3(grid_for(total, B)), dim3(B), 0, st, in, d_offs, nstreams, total, a);
@@ -303,18 +326,18 @@ int run_match_finder(Ctx* ctx, const Derived& d, const uint8_t* in, const uint64
     if (bt4) {
         {
             TimedLaunch tl(ctx, "mf_sort", st);
-            if ((rc = radix_sort(ctx, (uint32_t*)w.k2, (uint32_t*)w.ks, w.vals, w.vs, total, (int)(10 + sbits), st))) return rc;
+            if ((rc = segmented_sort(ctx, (uint32_t*)w.k2, (uint32_t*)w.ks, w.vals, w.vs, total, d_offs, nstreams, 10, st))) return rc;
         }
         hipLaunchKernelGGL(mf_prev_kernel, dim3(grid_for(total, B)), dim3(B), 0, st, (const uint32_t*)w.ks, w.vs, total, w.prev2);
         {
             TimedLaunch tl(ctx, "mf_sort", st);
-            if ((rc = radix_sort(ctx, (uint32_t*)w.k3, (uint32_t*)w.ks, w.vals, w.vs, total, (int)(16 + sbits), st))) return rc;
+            if ((rc = segmented_sort(ctx, (uint32_t*)w.k3, (uint32_t*)w.ks, w.vals, w.vs, total, d_offs, nstreams, 16, st))) return rc;
         }
         hipLaunchKernelGGL(mf_prev_kernel, dim3(grid_for(total, B)), dim3(B), 0, st, (const uint32_t*)w.ks, w.vs, total, w.prev3);
     }
     {
         TimedLaunch tl(ctx, "mf_sort", st);
-        if ((rc = radix_sort(ctx, w.k4, w.ks, w.vals, w.vs, total, (int)((bt4 ? d.hash_bits : 16) + sbits), st))) return rc;
+        if ((rc = segmented_sort(ctx, w.k4, w.ks, w.vals, w.vs, total, d_offs, nstreams, (int)(bt4 ? d.hash_bits : 16), st))) return rc;
     }
     hipMemsetAsync(w.counts, 0, 2 * sizeof(uint64_t), st);   // [0]=nvalid [1]=nchains
     hipLaunchKernelGGL(mf_heads_kernel, dim3(grid_for(total, B)), dim3(B), 0, st, w.ks, total, w.flag, w.counts);

@@ -1,5 +1,5 @@
-// TEST INFRASTRUCTURE ONLY -- CPU stand-ins for the two hipcub primitives the
-// runtime uses (stable radix sort by a bit range, flagged select), for the
+// TEST INFRASTRUCTURE ONLY -- CPU stand-ins for the hipcub primitives the
+// runtime uses (stable radix sort by a bit range, whole or per segment; flagged select), for the
 // SIMT emulation build in tests/simt. Not part of the product build.
 #pragma once
 #include <algorithm>
@@ -42,6 +42,21 @@ struct DeviceRadixSort {
     template <typename K, typename V, typename S>
     static int SortPairsDescending(void* tmp, size_t& bytes, const K* kin, K* kout, const V* vin, V* vout, int n, int b0, int b1, S) {
         return sort(tmp, bytes, kin, kout, vin, vout, n, b0, b1, true);
+    }
+};
+struct DeviceSegmentedRadixSort {
+    template <typename K, typename V, typename O, typename S>
+    static int SortPairs(void* tmp, size_t& bytes, const K* kin, K* kout, const V* vin, V* vout, int n, int nseg, O begin,
+                         O end, int b0, int b1, S s) {
+        if (!tmp) { bytes = 16; return 0; }
+        std::copy(kin, kin + n, kout);   // items outside every segment keep their place
+        std::copy(vin, vin + n, vout);
+        for (int g = 0; g < nseg; g++) {
+            const size_t lo = (size_t)begin[g], hi = (size_t)end[g];
+            if (hi > lo) DeviceRadixSort::sort(tmp, bytes, kin + lo, kout + lo, vin + lo, vout + lo, (int)(hi - lo), b0, b1, false);
+        }
+        (void)s;
+        return 0;
     }
 };
 struct DeviceSelect {
