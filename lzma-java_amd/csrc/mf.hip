@@ -72,14 +72,20 @@ __global__ void __launch_bounds__(256) mf_keys_kernel(const uint8_t* __restrict_
     }
 }
 
-// prev-in-bucket for a position-ordered sorted key array (hash2 / hash3 heads)
+// prev-in-bucket for a position-ordered sorted key array (hash2 / hash3 heads).
+// One item per thread, blocks mapped XCD-aware (XCD x takes the x-th eighth of
+// the array in order): the blocks resident on an XCD then scatter into a
+// fraction of one stream's prev[] range, so its L2 assembles whole lines
+// instead of writing back partial ones from all over the batch.
 __global__ void __launch_bounds__(256) mf_prev_kernel(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ vals,
                                                       uint64_t total, uint32_t* __restrict__ prev) {
-    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < total; i += (uint64_t)gridDim.x * blockDim.x) {
-        uint32_t k = keys[i];
-        if (k == kSentinel32) continue;
-        prev[vals[i]] = (i > 0 && keys[i - 1] == k) ? vals[i - 1] : kNoPos;
-    }
+    const uint32_t per_xcd = gridDim.x / 8;   // the host pads the grid to a multiple of 8
+    const uint64_t blk = (uint64_t)(blockIdx.x % 8) * per_xcd + blockIdx.x / 8;
+    const uint64_t i = blk * blockDim.x + threadIdx.x;
+    if (i >= total) return;
+    uint32_t k = keys[i];
+    if (k == kSentinel32) return;
+    prev[vals[i]] = (i > 0 && keys[i - 1] == k) ? vals[i - 1] : kNoPos;
 }
 
 // chain heads of the hash4 sort. The sorts are segmented per stream, so each
@@ -93,7 +99,8 @@ __global__ void __launch_bounds__(256) mf_heads_kernel(const uint64_t* __restric
     }
 }
 
-// chain lengths, and the walk-order key (stream ascending, length descending):
+// chain lengths, and the walk-order key (stream ascending, length descending,
+// lengths clamped at 1023: the order only shapes locality and lane balance):
 // the walk then works through the streams in order, so the lanes resident at
 // one time read a few streams' bytes (cache-resident) instead of the whole batch
 __global__ void __launch_bounds__(256) mf_chain_len_kernel(const uint32_t* __restrict__ starts, const uint64_t* __restrict__ nchains_p,
@@ -112,7 +119,7 @@ __global__ void __launch_bounds__(256) mf_chain_len_kernel(const uint32_t* __res
         const uint32_t len = (uint32_t)(e - starts[c]);
         lens[c] = len;
         const uint32_t stream = (uint32_t)(k >> key_shift);   // < 2^14 streams per pass
-        order_key[c] = (stream << 18) | (0x3FFFFu - (len < 0x3FFFFu ? len : 0x3FFFFu));
+        order_key[c] = (stream << 10) | (0x3FFu - (len < 0x3FFu ? len : 0x3FFu));   // 24 bits: 3 digit passes
     }
 }
 
@@ -324,16 +331,17 @@ int run_match_finder(Ctx* ctx, const Derived& d, const uint8_t* in, const uint64
     LZG_TRACE(ctx, st, "mf_keys done (%llu positions)", (unsigned long long)total);
     int rc;
     if (bt4) {
+        const unsigned prev_grid = (unsigned)(((total + B - 1) / B + 7) & ~7ull);   // total < 2^32: fits
         {
             TimedLaunch tl(ctx, "mf_sort", st);
             if ((rc = segmented_sort(ctx, (uint32_t*)w.k2, (uint32_t*)w.ks, w.vals, w.vs, total, d_offs, nstreams, 10, st))) return rc;
         }
-        hipLaunchKernelGGL(mf_prev_kernel, dim3(grid_for(total, B)), dim3(B), 0, st, (const uint32_t*)w.ks, w.vs, total, w.prev2);
+        hipLaunchKernelGGL(mf_prev_kernel, dim3(prev_grid), dim3(B), 0, st, (const uint32_t*)w.ks, w.vs, total, w.prev2);
         {
             TimedLaunch tl(ctx, "mf_sort", st);
             if ((rc = segmented_sort(ctx, (uint32_t*)w.k3, (uint32_t*)w.ks, w.vals, w.vs, total, d_offs, nstreams, 16, st))) return rc;
         }
-        hipLaunchKernelGGL(mf_prev_kernel, dim3(grid_for(total, B)), dim3(B), 0, st, (const uint32_t*)w.ks, w.vs, total, w.prev3);
+        hipLaunchKernelGGL(mf_prev_kernel, dim3(prev_grid), dim3(B), 0, st, (const uint32_t*)w.ks, w.vs, total, w.prev3);
     }
     {
         TimedLaunch tl(ctx, "mf_sort", st);
@@ -365,7 +373,7 @@ int run_match_finder(Ctx* ctx, const Derived& d, const uint8_t* in, const uint64
     {
         TimedLaunch tl(ctx, "mf_sort", st);
         hipLaunchKernelGGL(iota_kernel, dim3(grid_for(nchains, B)), dim3(B), 0, st, w.chain_idx, nchains);
-        if ((rc = radix_sort(ctx, okey, okey_sorted, w.chain_idx, w.chain_order, nchains, 32, st))) return rc;
+        if ((rc = radix_sort(ctx, okey, okey_sorted, w.chain_idx, w.chain_order, nchains, 24, st))) return rc;
     }
     hipMemsetAsync(w.ovf_used, 0, sizeof(unsigned long long), st);
     hipMemsetAsync(w.err, 0, sizeof(int), st);
