@@ -44,8 +44,13 @@ __device__ inline int find_stream(const uint64_t* offs, int nstreams, uint64_t g
 template <bool BT4>
 __global__ void __launch_bounds__(256) mf_keys_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ offs,
                                                       int nstreams, uint64_t total, MfArgs a) {
-    for (uint64_t g = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; g < total; g += (uint64_t)gridDim.x * blockDim.x) {
-        int s = find_stream(offs, nstreams, g);
+    // one position per thread; the block's first position gives a wave-uniform
+    // (scalar) stream search, and a lane past a stream end steps forward
+    const uint64_t g0 = blockIdx.x * (uint64_t)blockDim.x;
+    const uint64_t g = g0 + threadIdx.x;
+    int s = find_stream(offs, nstreams, g0 < total ? g0 : total - 1);
+    while (s + 1 < nstreams && offs[s + 1] <= g) s++;
+    if (g < total) {
         uint64_t base = offs[s], n = offs[s + 1] - base, p = g - base;
         a.minfo[g] = 0;
         a.vals[g] = (uint32_t)g;
@@ -54,7 +59,7 @@ __global__ void __launch_bounds__(256) mf_keys_kernel(const uint8_t* __restrict_
         if (len_limit < a.min_match_check) {   // BinTree.java:153-162: no insertion
             a.k4[g] = kSentinel;
             if (BT4) { a.k3[g] = kSentinel32; a.k2[g] = kSentinel32; }
-            continue;
+            return;
         }
         uint32_t b0 = in[g], b1 = in[g + 1];
         if (BT4) {
@@ -339,8 +344,9 @@ int run_match_finder(Ctx* ctx, const Derived& d, const uint8_t* in, const uint64
     const unsigned B = 256;
     {
         TimedLaunch tl(ctx, "mf_keys", st);
-        if (bt4) hipLaunchKernelGGL((mf_keys_kernel<true>), dim3(grid_for(total, B)), dim3(B), 0, st, in, d_offs, nstreams, total, a);
-        else hipLaunchKernelGGL((mf_keys_kernel<false>), dim3(grid_for(total, B)), dim3(B), 0, st, in, d_offs, nstreams, total, a);
+        const unsigned kgrid = (unsigned)((total + B - 1) / B);   // total < 2^32: fits
+        if (bt4) hipLaunchKernelGGL((mf_keys_kernel<true>), dim3(kgrid), dim3(B), 0, st, in, d_offs, nstreams, total, a);
+        else hipLaunchKernelGGL((mf_keys_kernel<false>), dim3(kgrid), dim3(B), 0, st, in, d_offs, nstreams, total, a);
     }
     LZG_TRACE(ctx, st, "mf_keys done (%llu positions)", (unsigned long long)total);
     int rc;
