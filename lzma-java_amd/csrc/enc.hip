@@ -1376,10 +1376,15 @@ __global__ void __launch_bounds__(kWave, 4) enc_kernel(EncArgs a) {
 #endif
 #ifdef LZG_PROF
     const uint64_t t_run = __builtin_amdgcn_s_memtime();
+    const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
 #endif
     e.run();
 #ifdef LZG_PROF
     e.prof[PF_TOTAL] = __builtin_amdgcn_s_memtime() - t_run;
+    e.prof[PF_T0] = rt0;   // 100 MHz wall clock: where each stream ran
+    e.prof[PF_T1] = __builtin_amdgcn_s_memrealtime();
+    // HW_REG_HW_ID (cu / sh / se / simd) and HW_REG_XCC_ID
+    e.prof[PF_HWID] = (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 4) | ((uint64_t)__builtin_amdgcn_s_getreg((15 << 11) | 20) << 32);
     if (e.lane == 0 && a.prof)
         for (int k = 0; k < kProfSlots; k++) a.prof[(size_t)s * kProfSlots + k] = e.prof[k];
 #endif

@@ -52,7 +52,7 @@ static void report_profile(const uint64_t* d_prof, int ns, uint64_t total, hipSt
     hipStreamSynchronize(st);
     static const char* names[kProfSlots] = {"total", "get_optimum", "match_lists", "rep_len", "two_step_len", "lit_price",
                                             "relax", "two_step_relax", "state", "backward", "encode", "tables",
-                                            "n_getopt", "n_positions"};
+                                            "n_getopt", "n_positions", "t0", "t1", "hwid"};
     double sum[kProfSlots] = {0};
     uint64_t mx = 0;
     for (int i = 0; i < ns; i++) {
@@ -61,9 +61,23 @@ static void report_profile(const uint64_t* d_prof, int ns, uint64_t total, hipSt
     }
     fprintf(stderr, "[lzg prof] %d streams, %llu bytes, max stream cycles %llu\n", ns, (unsigned long long)total,
             (unsigned long long)mx);
-    for (int k = 0; k < kProfSlots; k++)
+    for (int k = 0; k < PF_T0; k++)
         fprintf(stderr, "[lzg prof] %-15s %16.0f  %8.1f per byte  %5.1f%%\n", names[k], sum[k], sum[k] / (double)total,
                 k < PF_NOPT ? 100.0 * sum[k] / std::max(sum[0], 1.0) : 0.0);
+    // placement: wall-clock start/end per stream, grouped by CU (xcc, se, sh, cu)
+    if (getenv("LZG_PROF_DUMP")) {
+        FILE* f = fopen(getenv("LZG_PROF_DUMP"), "w");
+        if (f) {
+            fprintf(f, "stream,t0,t1,cycles,npos,hwid,xcc\n");
+            for (int i = 0; i < ns; i++) {
+                const uint64_t* r = &h[(size_t)i * kProfSlots];
+                fprintf(f, "%d,%llu,%llu,%llu,%llu,%u,%u\n", i, (unsigned long long)r[PF_T0], (unsigned long long)r[PF_T1],
+                        (unsigned long long)r[PF_TOTAL], (unsigned long long)r[PF_NPOS], (unsigned)(r[PF_HWID] & 0xFFFFFFFFu),
+                        (unsigned)(r[PF_HWID] >> 32));
+            }
+            fclose(f);
+        }
+    }
 }
 #endif
 
