@@ -270,7 +270,10 @@ struct Dec {
         int rc = LZMA_OK;
         // out_size >= 0: stop after out_size bytes (capped at 2^32 - 1, beyond any capacity)
         const uint32_t stop = out_size < 0 || out_size > 0xFFFFFFFFll ? 0xFFFFFFFFu : (uint32_t)out_size;
+        ProgressPrio prio;   // lzma_common.h: waves of a SIMD finish together
+        prio.start(stop);
         while (out_size < 0 || now < stop) {
+            prio.update(now);
             const uint32_t ps = now & ps_mask;
             // literal prefetch, issued before the isMatch decision: the coder's tree
             // (nodes 0-255) and, in matched mode, the 8 nodes along the match byte

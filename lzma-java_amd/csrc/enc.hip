@@ -179,6 +179,7 @@ struct Enc {
     uint32_t rd0, rd1, rd2, rd3;   // _repDistances
     uint32_t rp0, rp1, rp2, rp3;   // reps
     uint32_t match_price_count, align_price_count;
+    ProgressPrio prio;
     // ---- per-position gather (see gather()): p = current position, equality masks per side
     uint32_t gp;
     uint64_t gm0, gm1, gm2, gm3, gmp0, gmp1;
@@ -1232,6 +1233,7 @@ struct Enc {
         DBG(1, 4);
 
         uint32_t now_pos = 0;
+        prio.start(n);
         if (avail() == 0) { flush(0); return; }
         read_match_distances();
         DBG(1, 5);
@@ -1278,6 +1280,7 @@ struct Enc {
                 if (match_price_count >= (1u << 7)) fill_distances_prices();
                 if (align_price_count >= (uint32_t)kAlignTableSize) fill_align_prices();
                 PEND(PF_TABLES, tt);
+                prio.update(now_pos);
                 if (avail() == 0) { flush(now_pos); return; }
             }
         }

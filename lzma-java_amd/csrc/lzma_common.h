@@ -116,6 +116,40 @@ constexpr Tables make_tables() {
     return t;
 }
 
+// Wave priority by stream progress. The sequencer issues oldest-first among
+// waves of equal priority, so with one stream per wave the first two waves of
+// each SIMD run ahead and the last two finish alone at half occupancy (measured:
+// profiles/r01_enc_placement.txt). A wave lowers its priority (s_setprio 3..0)
+// as it passes 1/2, 3/4 and 7/8 of its stream: leaders then yield to laggards at
+// every threshold and the waves of a SIMD finish together.
+struct ProgressPrio {
+    uint32_t next, band, n;
+    __device__ inline void start(uint32_t len) {
+        n = len; band = 0; next = len >> 1;
+        set(0);
+    }
+    __device__ inline void update(uint32_t pos) {
+        if (pos < next || band >= 3) return;
+        while (band < 3 && pos >= next) {
+            band++;
+            next = band == 1 ? n - (n >> 2) : n - (n >> 3);
+        }
+        set(band);
+    }
+    __device__ static inline void set(uint32_t b) {
+#if LZG_WAVE == 64
+        switch (b) {
+            case 0: __builtin_amdgcn_s_setprio(3); break;
+            case 1: __builtin_amdgcn_s_setprio(2); break;
+            case 2: __builtin_amdgcn_s_setprio(1); break;
+            default: __builtin_amdgcn_s_setprio(0); break;
+        }
+#else
+        (void)b;
+#endif
+    }
+};
+
 // Everything the kernels derive from lzma_params (Encoder.java:1135-1180,
 // BinTree.java:59-134).
 struct Derived {
