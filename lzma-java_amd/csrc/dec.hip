@@ -50,6 +50,9 @@ DFI uint32_t vget(const uint32_t (&v)[kVS], uint32_t j) {
 }
 
 // PBS: posState stride of the probability layout (ProbLayout, lzma_common.h).
+// FairPrio rows of the decoder's waves (lzma_common.h)
+__device__ uint32_t g_dec_sched[kSchedRows * kSchedCols];
+
 template <int PBS>
 struct Dec {
     using PL = ProbLayout<PBS>;
@@ -270,10 +273,10 @@ struct Dec {
         int rc = LZMA_OK;
         // out_size >= 0: stop after out_size bytes (capped at 2^32 - 1, beyond any capacity)
         const uint32_t stop = out_size < 0 || out_size > 0xFFFFFFFFll ? 0xFFFFFFFFu : (uint32_t)out_size;
-        ProgressPrio prio;   // lzma_common.h: waves of a SIMD finish together
-        prio.start(stop);
+        FairPrio prio;   // lzma_common.h: the waves of a CU progress together
+        prio.start(g_dec_sched, stop, lane);
         while (out_size < 0 || now < stop) {
-            prio.update(now);
+            prio.update(now, lane);
             const uint32_t ps = now & ps_mask;
             // literal prefetch, issued before the isMatch decision: the coder's tree
             // (nodes 0-255) and, in matched mode, the 8 nodes along the match byte
@@ -386,6 +389,7 @@ struct Dec {
         }
         flush_to(now);
         *now_out = now;
+        prio.finish(lane);
         return rc;
     }
 };

@@ -114,6 +114,9 @@ FI uint32_t sel4(uint32_t i, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
     return i == 0 ? a : (i == 1 ? b : (i == 2 ? c : d));
 }
 
+// FairPrio rows of the encoder's waves (lzma_common.h)
+__device__ uint32_t g_enc_sched[kSchedRows * kSchedCols];
+
 template <typename PairT, bool LIT_LDS, int PBS>
 struct Enc {
     using PP = PairPack<PairT>;
@@ -179,7 +182,7 @@ struct Enc {
     uint32_t rd0, rd1, rd2, rd3;   // _repDistances
     uint32_t rp0, rp1, rp2, rp3;   // reps
     uint32_t match_price_count, align_price_count;
-    ProgressPrio prio;
+    FairPrio prio;
     // ---- per-position gather (see gather()): p = current position, equality masks per side
     uint32_t gp;
     uint64_t gm0, gm1, gm2, gm3, gmp0, gmp1;
@@ -1233,7 +1236,7 @@ struct Enc {
         DBG(1, 4);
 
         uint32_t now_pos = 0;
-        prio.start(n);
+        prio.start(g_enc_sched, n, lane);
         if (avail() == 0) { flush(0); return; }
         read_match_distances();
         DBG(1, 5);
@@ -1280,7 +1283,7 @@ struct Enc {
                 if (match_price_count >= (1u << 7)) fill_distances_prices();
                 if (align_price_count >= (uint32_t)kAlignTableSize) fill_align_prices();
                 PEND(PF_TABLES, tt);
-                prio.update(now_pos);
+                prio.update(now_pos, lane);
                 if (avail() == 0) { flush(now_pos); return; }
             }
         }
@@ -1382,6 +1385,7 @@ __global__ void __launch_bounds__(kWave, 4) enc_kernel(EncArgs a) {
     const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
 #endif
     e.run();
+    e.prio.finish(e.lane);
 #ifdef LZG_PROF
     e.prof[PF_TOTAL] = __builtin_amdgcn_s_memtime() - t_run;
     e.prof[PF_T0] = rt0;   // 100 MHz wall clock: where each stream ran

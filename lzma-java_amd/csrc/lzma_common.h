@@ -116,36 +116,60 @@ constexpr Tables make_tables() {
     return t;
 }
 
-// Wave priority by stream progress. The sequencer issues oldest-first among
-// waves of equal priority, so with one stream per wave the first two waves of
-// each SIMD run ahead and the last two finish alone at half occupancy (measured:
-// profiles/r01_enc_placement.txt). A wave lowers its priority (s_setprio 3..0)
-// as it passes 1/2, 3/4 and 7/8 of its stream: leaders then yield to laggards at
-// every threshold and the waves of a SIMD finish together.
-struct ProgressPrio {
-    uint32_t next, band, n;
-    __device__ inline void start(uint32_t len) {
-        n = len; band = 0; next = len >> 1;
-        set(0);
-    }
-    __device__ inline void update(uint32_t pos) {
-        if (pos < next || band >= 3) return;
-        while (band < 3 && pos >= next) {
-            band++;
-            next = band == 1 ? n - (n >> 2) : n - (n >> 3);
-        }
-        set(band);
-    }
-    __device__ static inline void set(uint32_t b) {
+// Fair wave priority for the one-stream-per-wave kernels. The sequencer issues
+// oldest-first among waves of equal priority, so the first two waves of each
+// SIMD run ahead and the last two finish alone at half occupancy (measured:
+// profiles/r01_enc_placement.txt). Every `step` bytes a wave publishes its
+// progress (fraction of its stream) in its CU's row of a per-kernel table,
+// reads the row back and sets s_setprio by its rank on the CU: the slowest
+// quarter gets priority 3, the fastest 0. Slots hold progress + 1, 0 = empty.
+// Table rows: 2048 CUs (xcc, se, sh, cu of HW_ID / XCC_ID) x 64 waves (simd, wave).
+constexpr uint32_t kSchedRows = 2048, kSchedCols = 64;
+struct FairPrio {
+    uint32_t* row;
+    uint32_t slot, next, step;
+    float scale;
+    __device__ inline void start(uint32_t* table, uint32_t len, uint32_t lane) {
 #if LZG_WAVE == 64
-        switch (b) {
+        const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);           // HW_REG_HW_ID
+        const uint32_t xcc = __builtin_amdgcn_s_getreg((15 << 11) | 20) & 7u;   // HW_REG_XCC_ID
+        const uint32_t cu = (((xcc * 8u + ((hw >> 13) & 7u)) * 2u + ((hw >> 12) & 1u)) * 16u) + ((hw >> 8) & 15u);
+        row = table + (size_t)cu * kSchedCols;
+        slot = ((hw >> 4) & 3u) * 16u + (hw & 15u);
+        step = len >> 8 > 256u ? len >> 8 : 256u;
+        next = step;
+        scale = 65536.0f / (float)(len ? len : 1u);
+        if (lane == 0) __hip_atomic_store(row + slot, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_amdgcn_s_setprio(3);
+#else
+        (void)table; (void)len; (void)lane;
+#endif
+    }
+    __device__ inline void update(uint32_t pos, uint32_t lane) {
+#if LZG_WAVE == 64
+        if (pos < next) return;
+        next = pos + step;
+        const uint32_t prog = (uint32_t)((float)pos * scale) + 1u;
+        if (lane == 0) __hip_atomic_store(row + slot, prog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t v = __hip_atomic_load(row + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t nact = (uint32_t)__builtin_popcountll(__ballot(v != 0u));
+        const uint32_t slower = (uint32_t)__builtin_popcountll(__ballot(v != 0u && v < prog));
+        const uint32_t q = nact ? (slower * 4u) / nact : 0u;   // 0: among the slowest quarter
+        switch (q) {
             case 0: __builtin_amdgcn_s_setprio(3); break;
             case 1: __builtin_amdgcn_s_setprio(2); break;
             case 2: __builtin_amdgcn_s_setprio(1); break;
             default: __builtin_amdgcn_s_setprio(0); break;
         }
 #else
-        (void)b;
+        (void)pos; (void)lane;
+#endif
+    }
+    __device__ inline void finish(uint32_t lane) {
+#if LZG_WAVE == 64
+        if (lane == 0) __hip_atomic_store(row + slot, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
+        (void)lane;
 #endif
     }
 };
