@@ -8,10 +8,9 @@
 // A position's tree only ever links positions of the same hash4 bucket, so
 // every bucket is an independent sequential simulation:
 //   K1 mf_keys     hash every position (BinTree.java:170-178), key = (stream, hv)
-//   K2 radix sort  stable, per stream (segmented) on hv => each bucket a
-//                  contiguous, position-ordered segment; hash2/hash3 likewise
-//   K3 mf_links    prev-in-bucket for hash2/hash3 (stored by hash4-sorted
-//                  index, the walk's visiting order); bucket (chain) heads
+//   K2 radix sort  (stream, hv) stable => each bucket a contiguous, position-
+//                  ordered segment; hash2/hash3 "last occurrence" likewise
+//   K3 mf_links    prev-in-bucket for hash2/hash3; bucket (chain) heads
 //   K4 mf_walk     one lane per bucket: replays BinTree.fillMatches0
 //                  (:152-273) for the bucket's positions in order, with the
 //                  son[] links indexed by sorted bucket index (window expiry
@@ -83,28 +82,15 @@ __global__ void __launch_bounds__(256) mf_keys_kernel(const uint8_t* __restrict_
 // the array in order): the blocks resident on an XCD then scatter into a
 // fraction of one stream's prev[] range, so its L2 assembles whole lines
 // instead of writing back partial ones from all over the batch.
-// prev[] is indexed by the position's hash4-sorted index (inv), so the walk
-// reads it in the order it visits positions.
 __global__ void __launch_bounds__(256) mf_prev_kernel(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ vals,
-                                                      const uint32_t* __restrict__ inv, uint64_t total,
-                                                      uint32_t* __restrict__ prev) {
+                                                      uint64_t total, uint32_t* __restrict__ prev) {
     const uint32_t per_xcd = gridDim.x / 8;   // the host pads the grid to a multiple of 8
     const uint64_t blk = (uint64_t)(blockIdx.x % 8) * per_xcd + blockIdx.x / 8;
     const uint64_t i = blk * blockDim.x + threadIdx.x;
     if (i >= total) return;
     uint32_t k = keys[i];
     if (k == kSentinel32) return;
-    prev[inv[vals[i]]] = (i > 0 && keys[i - 1] == k) ? vals[i - 1] : kNoPos;
-}
-
-// inv[position] = the position's index in the hash4-sorted order (XCD-aware like mf_prev)
-__global__ void __launch_bounds__(256) mf_inv_kernel(const uint32_t* __restrict__ vals, uint64_t total,
-                                                     uint32_t* __restrict__ inv) {
-    const uint32_t per_xcd = gridDim.x / 8;
-    const uint64_t blk = (uint64_t)(blockIdx.x % 8) * per_xcd + blockIdx.x / 8;
-    const uint64_t i = blk * blockDim.x + threadIdx.x;
-    if (i >= total) return;
-    inv[vals[i]] = (uint32_t)i;
+    prev[vals[i]] = (i > 0 && keys[i - 1] == k) ? vals[i - 1] : kNoPos;
 }
 
 // chain heads of the hash4 sort. The sorts are segmented per stream, so each
@@ -212,7 +198,7 @@ __global__ void __launch_bounds__(64) mf_walk_kernel(const uint8_t* __restrict__
         PairT* ov = nullptr;
         auto emit = [&](uint32_t l, uint32_t d) {
             if (cnt < kInlinePairs) {
-                // outputs are touched once: non-temporal, so the
+                // outputs and the hash2/3 links are touched once: non-temporal, so the
                 // stream's tree links and bytes keep the L2
                 __builtin_nontemporal_store(PP::pack(l, d), inl + cnt);
             } else {
@@ -227,7 +213,7 @@ __global__ void __launch_bounds__(64) mf_walk_kernel(const uint8_t* __restrict__
             cnt++;
         };
         if (BT4) {   // hash2 / hash3 candidates, BinTree.java:183-207
-            uint32_t pv2 = a.prev2[i], pv3 = a.prev3[i];   // by sorted index: a lane reads them in sequence
+            uint32_t pv2 = __builtin_nontemporal_load(a.prev2 + g), pv3 = __builtin_nontemporal_load(a.prev3 + g);
             uint32_t cm2 = pv2 == kNoPos ? 0 : (uint32_t)(pv2 - base) + 1;
             uint32_t cm3 = pv3 == kNoPos ? 0 : (uint32_t)(pv3 - base) + 1;
             if (cm2 > match_min && sb[cm2 - 1] == cur[0]) { max_len = 2; emit(2, pos - cm2 - 1); }
@@ -350,29 +336,22 @@ int run_match_finder(Ctx* ctx, const Derived& d, const uint8_t* in, const uint64
     }
     LZG_TRACE(ctx, st, "mf_keys done (%llu positions)", (unsigned long long)total);
     int rc;
+    if (bt4) {
+        const unsigned prev_grid = (unsigned)(((total + B - 1) / B + 7) & ~7ull);   // total < 2^32: fits
+        {
+            TimedLaunch tl(ctx, "mf_sort", st);
+            if ((rc = segmented_sort(ctx, (uint32_t*)w.k2, (uint32_t*)w.ks, w.vals, w.vs, total, d_offs, nstreams, 10, st))) return rc;
+        }
+        hipLaunchKernelGGL(mf_prev_kernel, dim3(prev_grid), dim3(B), 0, st, (const uint32_t*)w.ks, w.vs, total, w.prev2);
+        {
+            TimedLaunch tl(ctx, "mf_sort", st);
+            if ((rc = segmented_sort(ctx, (uint32_t*)w.k3, (uint32_t*)w.ks, w.vals, w.vs, total, d_offs, nstreams, 16, st))) return rc;
+        }
+        hipLaunchKernelGGL(mf_prev_kernel, dim3(prev_grid), dim3(B), 0, st, (const uint32_t*)w.ks, w.vs, total, w.prev3);
+    }
     {
         TimedLaunch tl(ctx, "mf_sort", st);
         if ((rc = segmented_sort(ctx, w.k4, w.ks, w.vals, w.vs, total, d_offs, nstreams, (int)(bt4 ? d.hash_bits : 16), st))) return rc;
-    }
-    if (bt4) {
-        // hash2 / hash3 heads, stored by hash4-sorted index (the order the walk
-        // visits positions in): inv maps a position to that index. The dead k4
-        // input keys hold the hash2 / hash3 sort outputs.
-        const unsigned xgrid = (unsigned)(((total + B - 1) / B + 7) & ~7ull);   // total < 2^32: fits
-        uint32_t* inv = w.inv;
-        uint32_t* sk = (uint32_t*)w.k4;
-        uint32_t* sv = sk + total;
-        hipLaunchKernelGGL(mf_inv_kernel, dim3(xgrid), dim3(B), 0, st, w.vs, total, inv);
-        {
-            TimedLaunch tl(ctx, "mf_sort", st);
-            if ((rc = segmented_sort(ctx, (uint32_t*)w.k2, sk, w.vals, sv, total, d_offs, nstreams, 10, st))) return rc;
-        }
-        hipLaunchKernelGGL(mf_prev_kernel, dim3(xgrid), dim3(B), 0, st, (const uint32_t*)sk, sv, inv, total, w.prev2);
-        {
-            TimedLaunch tl(ctx, "mf_sort", st);
-            if ((rc = segmented_sort(ctx, (uint32_t*)w.k3, sk, w.vals, sv, total, d_offs, nstreams, 16, st))) return rc;
-        }
-        hipLaunchKernelGGL(mf_prev_kernel, dim3(xgrid), dim3(B), 0, st, (const uint32_t*)sk, sv, inv, total, w.prev3);
     }
     hipMemsetAsync(w.counts, 0, 2 * sizeof(uint64_t), st);   // [0]=nvalid [1]=nchains
     hipLaunchKernelGGL(mf_heads_kernel, dim3(grid_for(total, B)), dim3(B), 0, st, w.ks, total, w.flag, w.counts);

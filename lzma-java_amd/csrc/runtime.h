@@ -33,7 +33,7 @@ struct MfBuffers {
     uint64_t *k4, *k3, *k2, *ks;
     uint32_t *vals, *vs, *minfo, *prev2, *prev3;
     uint8_t* flag;
-    uint32_t *chain_start, *chain_len, *inv, *chain_idx, *chain_order;   // inv: position -> hash4-sorted index
+    uint32_t *chain_start, *chain_len, *chain_len_sorted, *chain_idx, *chain_order;
     uint64_t* counts;
     uint32_t* son;
     void* pairs;

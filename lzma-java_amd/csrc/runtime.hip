@@ -123,7 +123,7 @@ static int encode_pass(Ctx* ctx, const Derived& d, const uint8_t* d_in, const ui
             w.vals = c.take<uint32_t>(T); w.vs = c.take<uint32_t>(T); w.minfo = c.take<uint32_t>(T);
             w.prev2 = c.take<uint32_t>(T); w.prev3 = c.take<uint32_t>(T);
             w.flag = c.take<uint8_t>(T);
-            w.chain_start = c.take<uint32_t>(T); w.chain_len = c.take<uint32_t>(T); w.inv = c.take<uint32_t>(T);
+            w.chain_start = c.take<uint32_t>(T); w.chain_len = c.take<uint32_t>(T); w.chain_len_sorted = c.take<uint32_t>(T);
             w.chain_idx = c.take<uint32_t>(T); w.chain_order = c.take<uint32_t>(T);
             w.counts = c.take<uint64_t>(2);
             w.son = c.take<uint32_t>(2 * T);
