@@ -1,15 +1,25 @@
-"""Benchmark: compress+decompress MB/s on 1 GiB of synthetic low-entropy data per GPU.
+"""Benchmark: compress+decompress MB/s on 1 GiB of synthetic data per job step.
 
-Workload (BASELINE.json metric / configs 2 and 4): the reference's own
-LzmaBench generator (LzmaBench.java:15-127), 1 GiB per rank, split into
-independent LZMA streams of --chunk bytes (default 256 KiB), each encoded
-exactly as Encoder.Code would with the level-5 mapping:
-dict 2^26, fb 32, BT4, lc3 lp0 pb2. A step = encode every stream (GPU),
-pack the outputs into one contiguous container (GPU), decode every stream
-(GPU). Inputs are resident in HBM before the timed region. Scaling is weak:
-each rank processes its own 1 GiB with no data-path collective; with N > 1
-ranks the step ends with the one exchange SURVEY.md 8(e) prescribes -- rank 0
-gathers every rank's packed streams over RCCL (lzma_amd.dist.gather_streams).
+Workload (BASELINE.json metric; configs 2-4): by default the reference's own
+LzmaBench generator (LzmaBench.java:15-127), 1 GiB, split into independent
+LZMA streams of --chunk bytes (default 256 KiB), each encoded exactly as
+Encoder.Code would with the level-5 mapping: dict 2^26,
+fb 32, BT4, lc3 lp0 pb2. `--data text` switches to the TEXT ("enwik9-shaped")
+generator at dict 2^28 (config 3). A step = encode every stream (GPU), pack
+the outputs into one contiguous buffer (GPU), decode every stream (GPU).
+Inputs are resident in HBM before the timed region.
+
+Multi-GPU: one process per GPU. Weak scaling (default):
+every rank encodes its own 1 GiB. Strong scaling (--strong, north_star's
+"one 1 GB buffer at 1, 2, 4 and 8 GPUs"): the 1 GiB buffer's streams are
+dealt round-robin, rank r taking {i : i mod G = r}. Either way there is no
+data-path collective; the step ends with the one exchange 8(e) prescribes:
+rank 0 gathers every rank's packed streams over RCCL.
+
+Parity: `verified` is true only if every stream decodes back to its input
+AND every sampled stream's GPU bytes equal the oracle's (the bit-exact C
+restatement of Encoder.Code) -- at N=1 the sample is the cpu_baseline's
+(spread over the whole buffer), at N>1 each rank checks its own sample.
 
 Prints ONE JSON line (rank 0).
 """
@@ -36,17 +46,43 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--size", type=int, default=1 << 30, help="uncompressed bytes per GPU")
+    ap.add_argument("--size", type=int, default=1 << 30, help="uncompressed bytes (per GPU; per job with --strong)")
     ap.add_argument("--chunk", type=int, default=256 << 10, help="bytes per independent stream")
+    ap.add_argument("--data", choices=["bench", "text"], default="bench",
+                    help="bench: LzmaBench generator (configs 2/4); text: enwik9-shaped TEXT (config 3)")
+    ap.add_argument("--dict-log", type=int, default=None, help="log2 dictionary size (default 26; 28 with --data text)")
+    ap.add_argument("--strong", action="store_true",
+                    help="strong scaling: one --size buffer, streams dealt round-robin over the ranks")
     ap.add_argument("--batch-bytes", type=int, default=1 << 30,
                     help="input bytes per device pass (1 GiB: all streams of a GPU in one encoder launch)")
-    ap.add_argument("--cpu-sample", type=int, default=32 << 20, help="bytes for the CPU baseline (0 = skip)")
-    ap.add_argument("--cpu-threads", type=int, default=16, help="threads for the multi-core CPU baseline")
+    ap.add_argument("--cpu-sample", type=int, default=128 << 20,
+                    help="bytes of the workload the multi-thread CPU baseline encodes+decodes (0 = skip)")
+    ap.add_argument("--cpu-single", type=int, default=8 << 20, help="bytes for the 1-thread CPU baseline")
+    ap.add_argument("--parity-streams", type=int, default=16,
+                    help="streams each rank checks against the oracle when there is no cpu_baseline sample")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--overlap", action="store_true",
                     help="pipeline the steps: the decode of step k runs on its own HIP stream and context while "
                          "step k+1 encodes (default: each step's encode and decode run back to back)")
     return ap.parse_args()
+
+
+def spread(n, k):
+    """k stream indices spread evenly over n streams (all of them when k >= n)."""
+    if k >= n:
+        return list(range(n))
+    return sorted(set(int(i) for i in np.linspace(0, n - 1, k).round()))
+
+
+def make_input(args, rank, world):
+    size = args.size
+    if args.data == "text":
+        seed = 1 if args.strong else 1 + rank
+        return lzma_amd.text_generate(size, seed)
+    host = lzma_amd.bench_generate(size)
+    if rank and not args.strong:   # distinct streams per rank: the generator output rotated by an odd offset
+        host = np.roll(host, -(rank * 262147) % size)
+    return host
 
 
 def main():
@@ -62,32 +98,40 @@ def main():
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
+    dict_log = args.dict_log if args.dict_log is not None else (28 if args.data == "text" else 26)
 
     # ---- synthetic data (host gen, then H2D; outside the timed region)
-    size = args.size
-    host = lzma_amd.bench_generate(size)
-    if rank:   # distinct streams per rank: the generator output rotated by a rank-dependent odd offset
-        host = np.roll(host, -(rank * 262147) % size)
+    full = make_input(args, rank, world)
+    size = full.size
+    n_all = (size + args.chunk - 1) // args.chunk
+    all_offs = np.minimum(np.arange(n_all + 1, dtype=np.uint64) * np.uint64(args.chunk), np.uint64(size))
+    mine = lzdist.rank_streams(n_all, rank, world) if args.strong else np.arange(n_all)
+    if args.strong:
+        host = np.concatenate([full[int(all_offs[i]):int(all_offs[i + 1])] for i in mine]) if mine.size else full[:0]
+    else:
+        host = full
+    my_size = int(host.size)
+    lens_in = (all_offs[1:] - all_offs[:-1])[mine]
+    n = int(mine.size)
+    offs = np.zeros(n + 1, dtype=np.uint64)
+    offs[1:] = np.cumsum(lens_in)
     d_in = torch.from_numpy(host).to(dev)
-    n = (size + args.chunk - 1) // args.chunk
-    offs = np.minimum(np.arange(n + 1, dtype=np.uint64) * np.uint64(args.chunk), np.uint64(size))
-    caps = np.array([lzma_amd.enc_bound(int(offs[i + 1] - offs[i])) for i in range(n)], dtype=np.uint64)
+    caps = np.array([lzma_amd.enc_bound(int(x)) for x in lens_in], dtype=np.uint64)
     cap_offs = np.zeros(n + 1, dtype=np.uint64)
     cap_offs[1:] = np.cumsum(caps)
-    d_comp = torch.empty(int(cap_offs[-1]), dtype=torch.uint8, device=dev)
+    d_comp = torch.empty(int(cap_offs[-1]) + 1, dtype=torch.uint8, device=dev)
     # two packed buffers: step k's decode reads one while step k+1 packs into the other
-    d_packs = [torch.empty(int(cap_offs[-1]), dtype=torch.uint8, device=dev) for _ in range(2)]
-    d_dec = torch.empty(size, dtype=torch.uint8, device=dev)
-    out_sizes = (offs[1:] - offs[:-1]).astype(np.int64)
+    d_packs = [torch.empty(int(cap_offs[-1]) + 1, dtype=torch.uint8, device=dev) for _ in range(2)]
+    d_dec = torch.empty(my_size + 1, dtype=torch.uint8, device=dev)
+    out_sizes = lens_in.astype(np.int64)
 
-    p = lzma_amd.make_params(dict_size=1 << 26, fb=32, mf=1, lc=3, lp=0, pb=2)
+    p = lzma_amd.make_params(dict_size=1 << dict_log, fb=32, mf=1, lc=3, lp=0, pb=2)
     props = lzma_amd.write_props(p)
     ctx = lzma_amd.Context(dev.index)
     ctx.set_batch_bytes(args.batch_bytes)
     st = torch.cuda.current_stream(dev).cuda_stream
     # the decoder gets its own context (its own device workspace) and HIP stream; with
-    # --overlap a step's decode runs while the next step encodes (measured: +3 %, the
-    # decoder and the match-finder sorts slow each other down). Every step still
+    # --overlap a step's decode runs while the next step encodes. Every step still
     # encodes and decodes all its bytes.
     ctx_dec = lzma_amd.Context(dev.index)
     dec_stream = torch.cuda.Stream(dev)
@@ -119,7 +163,7 @@ def main():
         if dist:   # the single data exchange: rank 0 collects every rank's packed streams
             g, _, _ = lzdist.gather_streams(buf, lens, dst=0)
             state["gathered"] = 0 if g is None else int(g.numel())
-        state["lens"] = lens
+        state["lens"], state["pk"], state["buf"] = lens, pk, buf
         state["t_enc"] = state.get("t_enc", 0.0) + (time.perf_counter() - t0)
         join()                           # one decode in flight at a time (d_dec is shared)
         if not args.overlap:
@@ -160,15 +204,40 @@ def main():
         elapsed = float(t.item())
 
     comp_bytes = int(np.sum(state["lens"]))
-    ok = bool((state["dstat"] == 0).all()) and bool((state["dlens"] == out_sizes).all())
+    roundtrip = bool((state["dstat"] == 0).all()) and bool((state["dlens"] == out_sizes).all())
     if not args.no_verify:
-        ok = ok and bool(torch.equal(d_dec, d_in))
-    if dist:
-        flag = torch.tensor([1 if ok else 0], device=dev)
-        torch.distributed.all_reduce(flag, op=torch.distributed.ReduceOp.MIN)
-        ok = bool(flag.item())
+        roundtrip = roundtrip and bool(torch.equal(d_dec[:my_size], d_in))
 
-    total_bytes = size * world * args.steps
+    # ---- CPU baseline (rank 0, N = 1) and the oracle parity sample
+    cpu, ref = None, {}
+    op = None
+    if not args.no_verify or (rank == 0 and world == 1 and args.cpu_sample > 0):
+        sys.path.insert(0, os.path.join(REPO, "tests"))
+        import oracle_ffi as orc
+        op = orc.params(p.dict_size, p.fb, p.mf, p.lc, p.lp, p.pb, p.eos)
+        chunks = [host[int(offs[i]):int(offs[i + 1])] for i in range(n)]
+        if rank == 0 and world == 1 and args.cpu_sample > 0:
+            cpu, ref = cpu_baseline(orc, op, chunks, args)
+        elif not args.no_verify:
+            idx = spread(n, args.parity_streams)
+            outs = orc.encode_many([chunks[i].tobytes() for i in idx], op, threads=min(4, orc.cpu_threads()))
+            ref = dict(zip(idx, outs))
+    parity_ok, checked = True, 0
+    if ref:
+        host_pack = state["buf"][:comp_bytes].cpu().numpy()
+        pk = state["pk"]
+        for i, r in ref.items():
+            checked += 1
+            if host_pack[int(pk[i]):int(pk[i + 1])].tobytes() != r:
+                parity_ok = False
+    ok = roundtrip and parity_ok and (checked > 0 or args.no_verify)
+    if dist:
+        flag = torch.tensor([1 if ok else 0, checked], device=dev, dtype=torch.int64)
+        torch.distributed.all_reduce(flag[:1], op=torch.distributed.ReduceOp.MIN)
+        torch.distributed.all_reduce(flag[1:], op=torch.distributed.ReduceOp.SUM)
+        ok, checked = bool(flag[0].item()), int(flag[1].item())
+
+    total_bytes = (size if args.strong else size * world) * args.steps
     value = total_bytes / elapsed / 1e6
 
     # ---- roofline for the dominant kernel (HIP events on the launch stream)
@@ -176,38 +245,39 @@ def main():
     dname, (dms, dlaunch) = dom
     avg_s = dms / 1e3 / max(dlaunch, 1)
     per_step_launches = max(dlaunch // max(args.steps, 1), 1)
-    if dname.startswith("dec"):
-        alg = (comp_bytes + size) / per_step_launches    # N_comp + N_out per launch
-    else:
-        alg = (size + comp_bytes) / per_step_launches    # N_in + N_out per launch
+    # compress: N_in + N_out per launch; decompress: N_comp + N_out (the same two numbers)
+    alg = (my_size + comp_bytes) / per_step_launches
     achieved = alg / avg_s if avg_s > 0 else 0.0
-    traffic, traffic_src = pmc_traffic(dname, args.size, args.chunk)
+    wl = {"bytes_per_gpu": args.size, "chunk": args.chunk, "data": args.data, "dict_log": dict_log}
+    traffic, traffic_src = pmc_traffic(dname, wl)
     roofline = {"bound": "hbm", "kernel": dname, "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
                 "unit": "GB/s", "frac": achieved / HBM_PEAK, "traffic": traffic, "traffic_source": traffic_src,
                 "avg_launch_ms": avg_s * 1e3, "launches_per_step": per_step_launches,
-                "alg_bytes_per_launch": alg}
-
-    cpu = None
-    if rank == 0 and args.cpu_sample > 0 and world == 1:
-        cpu = cpu_baseline(host, args.chunk, args.cpu_sample, p, args.cpu_threads)
+                "alg_bytes_per_launch": alg, "issue": issue_bound(dname, wl, avg_s, my_size)}
 
     if rank == 0:
+        desc = "LzmaBench generator" if args.data == "bench" else "TEXT (enwik9-shaped) generator"
         res = {
             "metric": "compress+decompress MB/s on 1 GB synthetic; bit-exact .lzma vs Java ref",
             "value": value, "unit": "MB/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "u8", "data": "synthetic (LzmaBench CBenchRandomGenerator)",
-            "config": {"workload": "LzmaBench generator %d MiB per GPU as %d independent streams of %d KiB; "
-                                   "dict 2^26 fb32 bt4 lc3 lp0 pb2 (level-5 mapping); encode+pack+decode"
-                                   % (size >> 20, n, args.chunk >> 10),
-                       "bytes_per_gpu": size, "chunk": args.chunk, "streams_per_gpu": n,
-                       "parallelism": "independent streams, %d rank(s)" % world},
-            "compress_MBps": size * world * args.steps / max(state["t_enc"], 1e-9) / 1e6,
-            "decompress_MBps": size * world * args.steps / max(state["t_dec"], 1e-9) / 1e6,
+            "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+            "scaling": "strong" if args.strong else "weak",
+            "vs_baseline": None, "dtype": "u8", "data": "synthetic (%s)" % desc,
+            "config": {"workload": "%s %d MiB %s as %d independent streams of %d KiB; dict 2^%d fb32 bt4 lc3 lp0 pb2 "
+                                   "(level-5 mapping); encode+pack+decode"
+                                   % (desc, size >> 20, "per job, dealt round-robin over the GPUs" if args.strong
+                                      else "per GPU", n_all, args.chunk >> 10, dict_log),
+                       "bytes_per_gpu": my_size, "chunk": args.chunk, "streams_per_gpu": n,
+                       "parallelism": "independent streams, %d rank(s)%s" % (world, ", round-robin" if args.strong else "")},
+            "compress_MBps": my_size * world * args.steps / max(state["t_enc"], 1e-9) / 1e6,
+            "decompress_MBps": my_size * world * args.steps / max(state["t_dec"], 1e-9) / 1e6,
             "schedule": "sequential" if not args.overlap else
                         "pipelined: step k's decode (own context + HIP stream) overlaps step k+1's encode; "
                         "compress/decompress MB/s are each phase's own wall time",
-            "ratio": comp_bytes / size, "verified": ok,
+            "ratio": comp_bytes / max(my_size, 1), "verified": ok,
+            "verified_means": "every stream decodes to its input and every sampled stream's bytes equal the "
+                              "oracle's Encoder.Code restatement",
+            "parity_streams_checked": checked, "roundtrip_ok": roundtrip,
             "gathered_bytes_rank0": state.get("gathered"),
             "kernels_ms": {k: {"total_ms": v[0], "launches": v[1]} for k, v in timings.items()},
             "roofline": roofline, "cpu_baseline": cpu,
@@ -225,18 +295,27 @@ def main():
 _KERNEL_OF = {"enc_parse": "enc_kernel", "dec_stream": "dec_kernel", "mf_walk": "mf_walk_kernel"}
 
 
-def pmc_traffic(label, size, chunk):
-    """HBM bytes per launch of the dominant kernel from the committed PMC
-    summary (profiles/traffic.json, written by tools/profile_round.sh from
-    separate FETCH_SIZE / WRITE_SIZE passes over this same workload), or None
-    when that summary is absent or was taken on another workload."""
-    path = os.path.join(REPO, "profiles", "traffic.json")
+def _profile(name, wl):
+    """A committed per-kernel summary from profiles/ (written by tools/profile_round.sh
+    over this same workload), or None when absent or taken on another workload."""
+    path = os.path.join(REPO, "profiles", name)
     if not os.path.exists(path):
-        return None, None
+        return None
     with open(path) as f:
         t = json.load(f)
     meta = t.get("_workload", {})
-    if meta.get("bytes_per_gpu") != size or meta.get("chunk") != chunk:
+    for k, v in wl.items():
+        if meta.get(k, {"data": "bench", "dict_log": 26}.get(k)) != v:
+            return None
+    return t
+
+
+def pmc_traffic(label, wl):
+    """HBM bytes per launch of the dominant kernel from profiles/traffic.json
+    (separate FETCH_SIZE / WRITE_SIZE passes; FETCH_SIZE doubled per the gfx950
+    correction of MI355X_MICROARCH.md)."""
+    t = _profile("traffic.json", wl)
+    if t is None:
         return None, None
     prefix = _KERNEL_OF.get(label, label)
     for k, v in t.items():
@@ -245,46 +324,83 @@ def pmc_traffic(label, size, chunk):
     return None, None
 
 
-def cpu_baseline(host, chunk, sample, p, threads):
-    """C restatement of the reference (oracle/) on a bounded sample of the same
-    chunks: encode + decode, MB/s of uncompressed bytes. Timed with 1 thread
-    (the reference is single-threaded) and with `threads` threads, one chunk
-    per task (ctypes releases the GIL inside the C calls); `value` is the
-    multi-thread figure."""
-    sys.path.insert(0, os.path.join(REPO, "tests"))
-    import oracle_ffi as orc
+def issue_bound(label, wl, avg_s, nbytes):
+    """The scalar-issue bound of the dominant kernel (the CU's single
+    scalar unit, not HBM, bounds the per-stream kernels): SQ_INSTS_SALU per CU over
+    (clock x kernel time), and instructions per input byte, from profiles/issue.json
+    (rocprofv3 --pmc SQ_INSTS_SALU SQ_INSTS_VALU ... over this workload)."""
+    t = _profile("issue.json", wl)
+    if t is None:
+        return None
+    prefix = _KERNEL_OF.get(label, label)
+    for k, v in t.items():
+        if k.startswith(prefix) and isinstance(v, dict) and "SQ_INSTS_SALU" in v:
+            cus, clk = t.get("_cus", 256), t.get("_sclk_hz", 2.4e9)
+            salu = v["SQ_INSTS_SALU"]
+            insts = v.get("SQ_INSTS_SALU", 0) + v.get("SQ_INSTS_VALU", 0) + v.get("SQ_INSTS_LDS", 0) + \
+                v.get("SQ_INSTS_VMEM", 0) + v.get("SQ_INSTS_SMEM", 0) + v.get("SQ_INSTS_BRANCH", 0)
+            return {"salu_per_cu": salu / cus, "salu_issue_frac": salu / cus / (clk * avg_s) if avg_s > 0 else None,
+                    "salu_per_input_byte": salu / max(nbytes, 1), "insts_per_input_byte": insts / max(nbytes, 1),
+                    "clock_hz": clk, "source": "profiles/issue.json (%s)" % k}
+    return None
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def cpu_baseline(orc, op, chunks, args):
+    """The oracle (bit-exact C restatement of Encoder.Code / Decoder.Code; there is
+    no JDK on the box) on a bounded sample of the same streams, as
+    SURVEY 8(d) prescribes: (i) 1 thread, (ii) the job's CPU share, one reused
+    encoder instance per thread (BinTree.Init clears the hash per Code call,
+    BinTree.java:72-80). MB/s of uncompressed bytes, encode then decode. Returns
+    the baseline block and the oracle bytes per sampled stream (the parity sample)."""
     from concurrent.futures import ThreadPoolExecutor
-    op = orc.params(p.dict_size, p.fb, p.mf, p.lc, p.lp, p.pb, p.eos)
     props = orc.props(op)
-    sample = min(sample, host.size)
-    chunks = [host[i:min(i + chunk, sample)].tobytes() for i in range(0, sample, chunk)]
+    n = len(chunks)
+    chunk = args.chunk
 
-    def enc(c):
-        return orc.encode(c, op)
+    def run(idx, threads):
+        data = [chunks[i].tobytes() for i in idx]
+        nbytes = sum(len(d) for d in data)
+        t0 = time.perf_counter()
+        encs = orc.encode_many(data, op, threads=threads)
+        t1 = time.perf_counter()
 
-    def dec(args):
-        c, e = args
-        rc, d = orc.decode(e, props, len(c))
-        assert rc == 1 and d == c
+        def dec(pair):
+            c, e = pair
+            rc, d = orc.decode(e, props, len(c))
+            return rc == 1 and d == c
+        with ThreadPoolExecutor(max_workers=threads) as ex:
+            good = all(ex.map(dec, zip(data, encs)))
+        t2 = time.perf_counter()
+        if not good:
+            raise RuntimeError("oracle round trip failed")
+        return encs, {"value": nbytes / (t2 - t0) / 1e6, "compress_MBps": nbytes / (t1 - t0) / 1e6,
+                      "decompress_MBps": nbytes / (t2 - t1) / 1e6, "bytes": nbytes, "streams": len(idx)}
 
-    def timed(nthreads):
-        with ThreadPoolExecutor(max_workers=nthreads) as ex:
-            t0 = time.perf_counter()
-            encs = list(ex.map(enc, chunks))
-            t1 = time.perf_counter()
-            list(ex.map(dec, zip(chunks, encs)))
-            t2 = time.perf_counter()
-        return sample / (t2 - t0) / 1e6, sample / (t1 - t0) / 1e6, sample / (t2 - t1) / 1e6
-
-    one = timed(1)
-    threads = max(1, min(threads, len(chunks)))
-    multi = timed(threads) if threads > 1 else one
-    return {"value": multi[0], "unit": "MB/s", "cores": threads, "kind": "port",
-            "compress_MBps": multi[1], "decompress_MBps": multi[2],
-            "single_thread": {"value": one[0], "compress_MBps": one[1], "decompress_MBps": one[2], "cores": 1},
-            "sample": "first %d MiB of the same workload (%d streams of %d KiB), oracle/ C restatement of the "
-                      "Java reference (no JDK on the box), %d threads; single_thread = 1 thread"
-                      % (sample >> 20, len(chunks), chunk >> 10, threads)}
+    threads = orc.cpu_threads()
+    one_idx = spread(n, max(1, args.cpu_single // chunk))
+    _, one = run(one_idx, 1)
+    multi_idx = spread(n, max(1, args.cpu_sample // chunk))
+    encs, multi = run(multi_idx, threads)
+    res = {"value": multi["value"], "unit": "MB/s", "cores": threads, "kind": "port",
+           "compress_MBps": multi["compress_MBps"], "decompress_MBps": multi["decompress_MBps"],
+           "cpu_model": cpu_model(), "cpus_visible": os.cpu_count(),
+           "single_thread": dict(one, cores=1),
+           "sample": "%d of the %d streams (%d MiB, spread evenly over the buffer), oracle/ C restatement of the "
+                     "Java reference (no JDK on the box), one reused encoder per thread, %d threads; "
+                     "single_thread: %d streams on 1 thread" % (len(multi_idx), n, multi["bytes"] >> 20, threads,
+                                                                len(one_idx))}
+    return res, dict(zip(multi_idx, encs))
 
 
 if __name__ == "__main__":

@@ -17,6 +17,7 @@
  *   lzma_pack_dev         (framing) contiguous multi-stream container
  *   lzma_decode           Decoder.Code (one stream)          Decoder.java:205-301
  *   lzma_dec_batch[_dev]  Decoder.Code on N independent streams
+ *   lzma_match_lists      BinTree.GetMatches at every position (diagnostic)  BinTree.java:152-273
  *   lzma_bench_generate   LzmaBench.CBenchRandomGenerator    LzmaBench.java:15-127
  *
  * Every encoded stream is byte-identical to Encoder.Code on the same bytes
@@ -111,9 +112,26 @@ int lzma_dec_batch(lzma_ctx *ctx, const uint8_t props[5],
 int lzma_decode(lzma_ctx *ctx, const uint8_t props[5], const uint8_t *in, uint64_t n,
                 int64_t out_size, uint8_t *out, uint64_t out_cap, uint64_t *out_len);
 
+/* ---- instrumented mode --------------------------------------
+ * The GPU match finder's per-position output for a batch of streams, as
+ * BinTree.GetMatches (BinTree.java:152-273) returns it at every position plus
+ * the ReadMatchDistances extension of the longest pair (Encoder.java:275-287):
+ * counts[g] pairs and main_len[g] for every input byte g (total = offs[n] -
+ * offs[0]), the pairs of all positions in order into lens/dists (at most
+ * cap; *total_pairs gets the full count, LZMA_E_OVERFLOW if it exceeds cap).
+ * A diagnostic for parity tests: the encoder consumes the same arrays. */
+int lzma_match_lists(lzma_ctx *ctx, const lzma_params *p, const uint8_t *in, const uint64_t *offs, int nstreams,
+                     uint32_t *counts, uint32_t *main_len, uint32_t *lens, uint32_t *dists, uint64_t cap,
+                     uint64_t *total_pairs);
+
 /* ---- synthetic inputs (bench / tests) ----------------------------------- */
 /* LzmaBench.CBenchRandomGenerator.Generate (LzmaBench.java:104-127). */
 void lzma_bench_generate(uint8_t *buf, uint64_t size);
+/* RND: SplitMix64 outputs, little-endian. */
+void lzma_rnd_generate(uint8_t *buf, uint64_t size, uint64_t seed);
+/* TEXT ("enwik9-shaped"): Zipf(1.1) words over a fixed
+ * 50k-word synthetic vocabulary with wiki-style markup about every 200 words. */
+void lzma_text_generate(uint8_t *buf, uint64_t size, uint64_t seed);
 
 #ifdef __cplusplus
 }

@@ -624,7 +624,7 @@ struct Enc {
         } else {
             LANE_FOR(uint32_t, k, 0u, cnt) {
                 PairT pr = k < (uint32_t)kInlinePairs ? ring_pairs[slot * kInlinePairs + k]
-                                                      : ovf[ovf_off[gbase + q] + k - kInlinePairs];
+                                                      : ovf[(uint64_t)ovf_off[gbase + q] * ovf_stride(fb) + k - kInlinePairs];
                 md_len[k] = (uint16_t)PP::len(pr);
                 md_dist[k] = PP::dist(pr);
             }

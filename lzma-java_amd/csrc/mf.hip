@@ -161,6 +161,7 @@ __global__ void __launch_bounds__(64) mf_walk_kernel(const uint8_t* __restrict__
                                                      MfArgs a, uint32_t* __restrict__ son, PairT* __restrict__ pairs,
                                                      uint32_t* __restrict__ ovf_off, PairT* __restrict__ ovf,
                                                      unsigned long long* __restrict__ ovf_used, uint64_t ovf_cap,
+                                                     uint32_t ovf_stride,
                                                      int* __restrict__ err) {
     using PP = PairPack<PairT>;
     uint64_t nchains = *nchains_p;
@@ -196,6 +197,10 @@ __global__ void __launch_bounds__(64) mf_walk_kernel(const uint8_t* __restrict__
         uint32_t max_len = 1, cnt = 0;
         PairT* inl = pairs + g * kInlinePairs;
         PairT* ov = nullptr;
+        bool ov_ok = false;
+        // the last emitted pair stays in registers: the fb extension below must not
+        // re-read it from memory (a failed overflow allocation leaves no copy there)
+        uint32_t last_l = 0, last_d = 0;
         auto emit = [&](uint32_t l, uint32_t d) {
             if (cnt < kInlinePairs) {
                 // outputs and the hash2/3 links are touched once: non-temporal, so the
@@ -203,13 +208,18 @@ __global__ void __launch_bounds__(64) mf_walk_kernel(const uint8_t* __restrict__
                 __builtin_nontemporal_store(PP::pack(l, d), inl + cnt);
             } else {
                 if (ov == nullptr) {
-                    unsigned long long o = atomicAdd(ovf_used, (unsigned long long)(fb + 2));
-                    if (o + fb + 2 > ovf_cap) { *err = 1; o = 0; }
+                    // the pool is handed out in slots of ovf_stride pairs: a position
+                    // takes at most one slot, so a 32-bit slot index always suffices
+                    unsigned long long o = atomicAdd(ovf_used, 1ull);
+                    ov_ok = (o + 1) * ovf_stride <= ovf_cap;
+                    if (!ov_ok) { *err = 1; o = 0; }
                     ovf_off[g] = (uint32_t)o;
-                    ov = ovf + o;
+                    ov = ovf + o * ovf_stride;
                 }
-                if (!*err) ov[cnt - kInlinePairs] = PP::pack(l, d);
+                if (ov_ok) ov[cnt - kInlinePairs] = PP::pack(l, d);
             }
+            last_l = l;
+            last_d = d;
             cnt++;
         };
         if (BT4) {   // hash2 / hash3 candidates, BinTree.java:183-207
@@ -217,13 +227,18 @@ __global__ void __launch_bounds__(64) mf_walk_kernel(const uint8_t* __restrict__
             uint32_t cm2 = pv2 == kNoPos ? 0 : (uint32_t)(pv2 - base) + 1;
             uint32_t cm3 = pv3 == kNoPos ? 0 : (uint32_t)(pv3 - base) + 1;
             if (cm2 > match_min && sb[cm2 - 1] == cur[0]) { max_len = 2; emit(2, pos - cm2 - 1); }
+            const uint32_t d2 = pos - cm2 - 1;   // the len-2 pair's distance, if it was emitted
             if (cm3 > match_min && sb[cm3 - 1] == cur[0]) {
                 if (cm3 == cm2) cnt--;
                 max_len = 3;
                 emit(3, pos - cm3 - 1);
                 cm2 = cm3;
             }
-            if (cnt != 0 && cm2 == cur_match) { cnt--; max_len = 1; }
+            if (cnt != 0 && cm2 == cur_match) {
+                cnt--;
+                max_len = 1;
+                if (cnt == 1) { last_l = 2; last_d = d2; }   // the len-2 pair is the last one again
+            }
         }
         uint64_t ptr0 = 2 * i + 1, ptr1 = 2 * i;
         uint64_t cur_idx = i - 1;           // sorted index of the head (valid while cur_match != 0)
@@ -254,10 +269,9 @@ __global__ void __launch_bounds__(64) mf_walk_kernel(const uint8_t* __restrict__
         }
         uint32_t ml = 0;
         if (cnt > 0) {   // Encoder.ReadMatchDistances extension, Encoder.java:279-284
-            PairT last = cnt <= kInlinePairs ? inl[cnt - 1] : ov[cnt - 1 - kInlinePairs];
-            ml = PP::len(last);
+            ml = last_l;
             if (ml == fb) {
-                uint32_t d1 = PP::dist(last) + 1;
+                uint32_t d1 = last_d + 1;
                 uint64_t from = (uint64_t)p + ml;
                 uint64_t lim = kMatchMaxLen - ml;
                 if (from + lim > n) lim = n - from;
@@ -389,11 +403,11 @@ int run_match_finder(Ctx* ctx, const Derived& d, const uint8_t* in, const uint64
         unsigned grid = (unsigned)((nchains + WB - 1) / WB);
         grid = (grid + 7) & ~7u;   // multiple of 8 (XCD-aware mapping in mf_walk_kernel)
         if (wide_pairs) {
-            if (bt4) hipLaunchKernelGGL((mf_walk_kernel<uint64_t, true>), dim3(grid), dim3(WB), 0, st, in, d_offs, w.ks, w.vs, w.chain_order, w.chain_start, w.chain_len, w.counts + 1, a, w.son, (uint64_t*)w.pairs, w.ovf_off, (uint64_t*)w.ovf, w.ovf_used, w.ovf_cap, w.err);
-            else hipLaunchKernelGGL((mf_walk_kernel<uint64_t, false>), dim3(grid), dim3(WB), 0, st, in, d_offs, w.ks, w.vs, w.chain_order, w.chain_start, w.chain_len, w.counts + 1, a, w.son, (uint64_t*)w.pairs, w.ovf_off, (uint64_t*)w.ovf, w.ovf_used, w.ovf_cap, w.err);
+            if (bt4) hipLaunchKernelGGL((mf_walk_kernel<uint64_t, true>), dim3(grid), dim3(WB), 0, st, in, d_offs, w.ks, w.vs, w.chain_order, w.chain_start, w.chain_len, w.counts + 1, a, w.son, (uint64_t*)w.pairs, w.ovf_off, (uint64_t*)w.ovf, w.ovf_used, w.ovf_cap, ovf_stride(d.fb), w.err);
+            else hipLaunchKernelGGL((mf_walk_kernel<uint64_t, false>), dim3(grid), dim3(WB), 0, st, in, d_offs, w.ks, w.vs, w.chain_order, w.chain_start, w.chain_len, w.counts + 1, a, w.son, (uint64_t*)w.pairs, w.ovf_off, (uint64_t*)w.ovf, w.ovf_used, w.ovf_cap, ovf_stride(d.fb), w.err);
         } else {
-            if (bt4) hipLaunchKernelGGL((mf_walk_kernel<uint32_t, true>), dim3(grid), dim3(WB), 0, st, in, d_offs, w.ks, w.vs, w.chain_order, w.chain_start, w.chain_len, w.counts + 1, a, w.son, (uint32_t*)w.pairs, w.ovf_off, (uint32_t*)w.ovf, w.ovf_used, w.ovf_cap, w.err);
-            else hipLaunchKernelGGL((mf_walk_kernel<uint32_t, false>), dim3(grid), dim3(WB), 0, st, in, d_offs, w.ks, w.vs, w.chain_order, w.chain_start, w.chain_len, w.counts + 1, a, w.son, (uint32_t*)w.pairs, w.ovf_off, (uint32_t*)w.ovf, w.ovf_used, w.ovf_cap, w.err);
+            if (bt4) hipLaunchKernelGGL((mf_walk_kernel<uint32_t, true>), dim3(grid), dim3(WB), 0, st, in, d_offs, w.ks, w.vs, w.chain_order, w.chain_start, w.chain_len, w.counts + 1, a, w.son, (uint32_t*)w.pairs, w.ovf_off, (uint32_t*)w.ovf, w.ovf_used, w.ovf_cap, ovf_stride(d.fb), w.err);
+            else hipLaunchKernelGGL((mf_walk_kernel<uint32_t, false>), dim3(grid), dim3(WB), 0, st, in, d_offs, w.ks, w.vs, w.chain_order, w.chain_start, w.chain_len, w.counts + 1, a, w.son, (uint32_t*)w.pairs, w.ovf_off, (uint32_t*)w.ovf, w.ovf_used, w.ovf_cap, ovf_stride(d.fb), w.err);
         }
     }
     LZG_TRACE(ctx, st, "mf_walk done (%llu chains)", (unsigned long long)nchains);

@@ -65,7 +65,7 @@ struct Ctx {
     size_t arena_size = 0;
     uint8_t* tmp = nullptr;     // cub temp storage
     size_t tmp_size = 0;
-    uint64_t ovf_hint = 0;      // overflow pool slots per byte * 1024 (grows on retry)
+    uint64_t ovf_hint = 0;      // overflow pool slots per 1024 input bytes (0 = default; grows on retry)
     // timing
     bool timing = false;
     struct Pending { std::string name; hipEvent_t a, b; };
@@ -206,6 +206,10 @@ struct Carver {
 };
 
 __global__ void iota_kernel(uint32_t* out, uint64_t n);
+
+// overflow pool slot: pairs beyond the inline ones of one position (at most
+// fb - 1 pairs per position: lengths 2..fb, strictly increasing)
+__host__ __device__ inline uint32_t ovf_stride(uint32_t fb) { return fb > (uint32_t)kInlinePairs + 1 ? fb - 1 - kInlinePairs : 1u; }
 
 int run_match_finder(Ctx* ctx, const Derived& d, const uint8_t* in, const uint64_t* d_offs, int nstreams,
                      uint64_t total, bool wide_pairs, MfBuffers& w, hipStream_t st);

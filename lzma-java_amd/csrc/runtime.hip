@@ -85,10 +85,20 @@ static void report_profile(const uint64_t* d_prof, int ns, uint64_t total, hipSt
 // 16384 streams (~2.6 GB).
 constexpr int kMaxStreamsPerPass = 16384;
 
-// one encode pass over streams [s0, s1) of a batch
+// Host copies of the match finder's per-position output (the instrumented
+// mode of SURVEY 7.1: lzma_match_lists diffs them against the oracle).
+struct MatchDump {
+    std::vector<uint32_t> minfo, ovf_off;
+    std::vector<uint8_t> pairs, ovf;
+    bool wide = false;
+    uint32_t stride = 0;
+};
+
+// one encode pass over streams [s0, s1) of a batch (dump != null: stop after
+// the match finder and copy its output to the host)
 static int encode_pass(Ctx* ctx, const Derived& d, const uint8_t* d_in, const uint64_t* h_offs, int s0, int s1,
                        uint8_t* d_out, const uint64_t* h_out_offs, uint64_t* h_out_lens, int32_t* h_status,
-                       hipStream_t st) {
+                       hipStream_t st, MatchDump* dump = nullptr) {
     const int ns = s1 - s0;
     const uint64_t in0 = h_offs[s0];
     const uint64_t total = h_offs[s1] - in0;
@@ -106,8 +116,16 @@ static int encode_pass(Ctx* ctx, const Derived& d, const uint8_t* d_in, const ui
     });
     const int grid = enc_grid(d, ns);
     const size_t scr = (enc_scratch_per_block(d) + 255) & ~(size_t)255;
-    uint64_t ovf_cap = total * std::max<uint64_t>(1, (d.fb + 2) / 16) + 65536;
-    if (ctx->ovf_hint > ovf_cap) ovf_cap = ctx->ovf_hint;
+    // overflow pool in slots of ovf_stride(fb) pairs, one slot per position with more
+    // than kInlinePairs pairs: start at 1 slot per 16 positions (a retry grows it 4x and
+    // remembers the rate for later passes of this context), never more than one per position
+    const uint64_t stride = ovf_stride(d.fb);
+    uint64_t slots_per_k = std::max<uint64_t>(64, ctx->ovf_hint);
+    auto pool_cap = [&](uint64_t spk) {
+        uint64_t slots = std::min<uint64_t>(total, (total * spk + 1023) / 1024) + 64;
+        return slots * stride;
+    };
+    uint64_t ovf_cap = pool_cap(slots_per_k);
     for (int attempt = 0; attempt < 6; attempt++) {
         const uint64_t T = total;
         auto need = [&](Carver& c, MfBuffers& w, uint8_t** inpad, uint64_t** d_offs, uint64_t** d_oofs,
@@ -159,11 +177,32 @@ static int encode_pass(Ctx* ctx, const Derived& d, const uint8_t* d_in, const ui
         }
         int rc = run_match_finder(ctx, d, inpad, d_offs, ns, total, wide, w, st);
         if (rc == LZMA_E_OVERFLOW) {
-            ovf_cap *= 4;
-            ctx->ovf_hint = ovf_cap;
+            if (slots_per_k >= 1024) return ctx->fail(LZMA_E_INTERNAL, "overflow pool full at one slot per position");
+            slots_per_k = std::min<uint64_t>(1024, slots_per_k * 4);
+            ctx->ovf_hint = slots_per_k;
+            ovf_cap = pool_cap(slots_per_k);
             continue;
         }
         if (rc) return rc;
+        if (dump) {
+            dump->wide = wide;
+            dump->stride = (uint32_t)stride;
+            dump->minfo.resize(total);
+            dump->ovf_off.resize(total);
+            dump->pairs.resize(total * kInlinePairs * psz);
+            unsigned long long used = 0;
+            HIPCHK(hipMemcpyAsync(&used, w.ovf_used, sizeof used, hipMemcpyDeviceToHost, st));
+            HIPCHK(hipStreamSynchronize(st));
+            dump->ovf.resize(std::min<uint64_t>(used * stride, ovf_cap) * psz);
+            if (total) {
+                HIPCHK(hipMemcpyAsync(dump->minfo.data(), w.minfo, total * 4, hipMemcpyDeviceToHost, st));
+                HIPCHK(hipMemcpyAsync(dump->ovf_off.data(), w.ovf_off, total * 4, hipMemcpyDeviceToHost, st));
+                HIPCHK(hipMemcpyAsync(dump->pairs.data(), w.pairs, dump->pairs.size(), hipMemcpyDeviceToHost, st));
+            }
+            if (!dump->ovf.empty()) HIPCHK(hipMemcpyAsync(dump->ovf.data(), w.ovf, dump->ovf.size(), hipMemcpyDeviceToHost, st));
+            HIPCHK(hipStreamSynchronize(st));
+            return LZMA_OK;
+        }
         EncArgs a{};
         a.in = inpad; a.offs = d_offs; a.order = d_order; a.nstreams = ns; a.next = d_next;
         a.minfo = w.minfo; a.pairs = w.pairs; a.ovf_off = w.ovf_off; a.ovf = w.ovf;
@@ -238,9 +277,12 @@ static int decode_batch_dev(Ctx* ctx, const uint8_t props[5], const uint8_t* d_i
     lzma_params p;
     if (lzma_read_props(props, &p) != LZMA_OK) return ctx->fail(LZMA_E_PARAM, "bad properties (Decoder.SetDecoderProperties false)");
     if (nstreams <= 0) return nstreams == 0 ? LZMA_OK : ctx->fail(LZMA_E_PARAM, "nstreams < 0");
-    for (int i = 0; i < nstreams; i++)   // the decoder kernel keeps 32-bit input positions
+    for (int i = 0; i < nstreams; i++) {   // the decoder kernel keeps 32-bit input positions
         if (h_in_offs[i + 1] < h_in_offs[i] || h_in_offs[i + 1] - h_in_offs[i] >= 0xFFFFFFFFull)
             return ctx->fail(LZMA_E_PARAM, "compressed stream %d: bad offsets or >= 4 GiB", i);
+        if (h_out_offs[i + 1] < h_out_offs[i] || h_out_offs[i + 1] - h_out_offs[i] >= 0xFFFFFFFFull)
+            return ctx->fail(LZMA_E_PARAM, "output region %d: offsets not monotone or >= 4 GiB", i);
+    }
     uint32_t dict = (uint32_t)props[1] | ((uint32_t)props[2] << 8) | ((uint32_t)props[3] << 16) | ((uint32_t)props[4] << 24);
     const uint32_t lc = (uint32_t)p.lc, lp = (uint32_t)p.lp, pb = (uint32_t)p.pb;
     const uint32_t lit_lds = 0;   // literal coders always in the per-stream HBM scratch (dec.hip)
@@ -462,6 +504,62 @@ int lzma_enc_batch(lzma_ctx* ctx, const lzma_params* p, const uint8_t* in, const
 done:
     hipFree(d_in); hipFree(d_out); hipFree(d_pack); hipFree(d_co); hipFree(d_po);
     return rc;
+}
+
+int lzma_match_lists(lzma_ctx* ctx, const lzma_params* p, const uint8_t* in, const uint64_t* offs, int nstreams,
+                     uint32_t* counts, uint32_t* main_len, uint32_t* lens, uint32_t* dists, uint64_t cap,
+                     uint64_t* total_pairs) {
+    if (!ctx || !p || !offs || nstreams < 0 || !counts || !main_len || !total_pairs) return LZMA_E_PARAM;
+    if (check_device(ctx)) return LZMA_E_NODEVICE;
+    hipSetDevice(ctx->device);
+    Derived d;
+    if (derive(*p, d) != LZMA_OK) return ctx->fail(LZMA_E_PARAM, "invalid lzma_params");
+    *total_pairs = 0;
+    if (nstreams == 0) return LZMA_OK;
+    const uint64_t total = offs[nstreams] - offs[0];
+    if (total >= (1ull << 31)) return ctx->fail(LZMA_E_PARAM, "match-list dump is limited to one pass (< 2 GiB)");
+    std::vector<uint64_t> rel(nstreams + 1), oo(nstreams + 1, 0), lens_h(nstreams);
+    std::vector<int32_t> status(nstreams);
+    for (int i = 0; i <= nstreams; i++) {
+        rel[i] = offs[i] - offs[0];
+        if (i && rel[i] < rel[i - 1]) return ctx->fail(LZMA_E_PARAM, "offsets not monotone");
+    }
+    uint8_t* d_in = nullptr;
+    if (hipMalloc(&d_in, total + 1) != hipSuccess) return ctx->fail(LZMA_E_NOMEM, "device input");
+    if (total && hipMemcpy(d_in, in + offs[0], total, hipMemcpyHostToDevice) != hipSuccess) {
+        hipFree(d_in);
+        return ctx->fail(LZMA_E_DEVICE, "H2D");
+    }
+    MatchDump dump;
+    int rc = encode_pass(ctx, d, d_in, rel.data(), 0, nstreams, nullptr, oo.data(), lens_h.data(), status.data(),
+                         nullptr, &dump);
+    hipFree(d_in);
+    if (rc) return rc;
+    uint64_t k = 0;
+    for (uint64_t g = 0; g < total; g++) {
+        const uint32_t info = dump.minfo[g], cnt = info & 0xFFFFu;
+        counts[g] = cnt;
+        main_len[g] = info >> 16;
+        for (uint32_t j = 0; j < cnt; j++, k++) {
+            uint64_t pr;
+            const uint64_t idx = j < (uint32_t)kInlinePairs ? g * kInlinePairs + j
+                                                            : (uint64_t)dump.ovf_off[g] * dump.stride + j - kInlinePairs;
+            const std::vector<uint8_t>& src = j < (uint32_t)kInlinePairs ? dump.pairs : dump.ovf;
+            if (dump.wide) {
+                if ((idx + 1) * 8 > src.size()) return ctx->fail(LZMA_E_INTERNAL, "pair index out of range");
+                memcpy(&pr, &src[idx * 8], 8);
+            } else {
+                uint32_t v;
+                if ((idx + 1) * 4 > src.size()) return ctx->fail(LZMA_E_INTERNAL, "pair index out of range");
+                memcpy(&v, &src[idx * 4], 4);
+                pr = ((uint64_t)(v >> 23) << 32) | (v & 0x7FFFFFu);
+            }
+            if (k < cap && lens && dists) { lens[k] = (uint32_t)(pr >> 32); dists[k] = (uint32_t)pr; }
+        }
+    }
+    *total_pairs = k;
+    if (k > cap) return ctx->fail(LZMA_E_OVERFLOW, "%llu pairs > cap %llu", (unsigned long long)k, (unsigned long long)cap);
+    return LZMA_OK;
 }
 
 int lzma_encode(lzma_ctx* ctx, const lzma_params* p, const uint8_t* in, uint64_t n, uint8_t* out, uint64_t out_cap,

@@ -41,6 +41,7 @@ EXPORTED_SYMBOLS = [
     "lzma_ctx_set_timing", "lzma_ctx_timings", "lzma_ctx_reset_timings", "lzma_enc_batch_dev", "lzma_enc_batch",
     "lzma_pack_dev",
     "lzma_encode", "lzma_dec_batch_dev", "lzma_dec_batch", "lzma_decode", "lzma_bench_generate",
+    "lzma_rnd_generate", "lzma_text_generate", "lzma_match_lists",
 ]
 
 
@@ -104,6 +105,11 @@ def lib():
         L.lzma_decode.argtypes = [vp, vp, vp, u64, ctypes.c_int64, vp, u64, ctypes.POINTER(u64)]
         L.lzma_bench_generate.argtypes = [vp, u64]
         L.lzma_bench_generate.restype = None
+        L.lzma_match_lists.argtypes = [vp, P, vp, vp, i32, vp, vp, vp, vp, u64, ctypes.POINTER(u64)]
+        L.lzma_rnd_generate.argtypes = [vp, u64, u64]
+        L.lzma_rnd_generate.restype = None
+        L.lzma_text_generate.argtypes = [vp, u64, u64]
+        L.lzma_text_generate.restype = None
         _lib_handle = L
     return _lib_handle
 
@@ -147,6 +153,31 @@ def bench_generate(size: int) -> np.ndarray:
     buf = np.empty(max(size, 1), dtype=np.uint8)
     lib().lzma_bench_generate(buf.ctypes.data, size)
     return buf[:size]
+
+
+def rnd_generate(size: int, seed: int = 0x5EED) -> np.ndarray:
+    """RND input of SURVEY.md 8(d): SplitMix64 bytes (config 1: 1 MiB, seed 0x5EED)."""
+    buf = np.empty(max(size, 1), dtype=np.uint8)
+    lib().lzma_rnd_generate(buf.ctypes.data, size, seed)
+    return buf[:size]
+
+
+def text_generate(size: int, seed: int = 1) -> np.ndarray:
+    """TEXT ("enwik9-shaped") input of SURVEY.md 8(d): Zipf(1.1) words, wiki markup (config 3: seed 1)."""
+    buf = np.empty(max(size, 1), dtype=np.uint8)
+    lib().lzma_text_generate(buf.ctypes.data, size, seed)
+    return buf[:size]
+
+
+def generate(kind: str, size: int) -> np.ndarray:
+    """Synthetic input by name: 'bench' (LzmaBench), 'text' (config 3) or 'rnd' (config 1)."""
+    if kind == "bench":
+        return bench_generate(size)
+    if kind == "text":
+        return text_generate(size)
+    if kind == "rnd":
+        return rnd_generate(size)
+    raise ValueError("unknown input kind %r" % kind)
 
 
 class Context:
@@ -232,6 +263,31 @@ class Context:
             L = min(int(lens[i]), int(oo[i + 1] - oo[i]))
             res.append((int(status[i]), out[oo[i]:oo[i] + L].tobytes()))
         return res
+
+    def match_lists(self, streams: Sequence[bytes], p: Params):
+        """The GPU match finder's output (lzma_match_lists): per input byte of the
+        concatenated streams (count, main_len), and all pairs in position order."""
+        arrs = [np.frombuffer(s, dtype=np.uint8) if not isinstance(s, np.ndarray) else s for s in streams]
+        offs = np.zeros(len(arrs) + 1, dtype=np.uint64)
+        np.cumsum([a.size for a in arrs], out=offs[1:])
+        data = np.concatenate(arrs) if arrs and offs[-1] > 0 else np.zeros(1, dtype=np.uint8)
+        n = int(offs[-1])
+        counts = np.zeros(max(n, 1), dtype=np.uint32)
+        main = np.zeros(max(n, 1), dtype=np.uint32)
+        cap = max(n * 4, 64)
+        while True:
+            lens = np.zeros(cap, dtype=np.uint32)
+            dists = np.zeros(cap, dtype=np.uint32)
+            tot = ctypes.c_uint64()
+            rc = lib().lzma_match_lists(self.h, ctypes.byref(p), data.ctypes.data, offs.ctypes.data, len(arrs),
+                                        counts.ctypes.data, main.ctypes.data, lens.ctypes.data, dists.ctypes.data,
+                                        cap, ctypes.byref(tot))
+            if rc == LZMA_E_OVERFLOW:
+                cap = int(tot.value)
+                continue
+            self.check(rc)
+            k = int(tot.value)
+            return counts[:n], main[:n], lens[:k], dists[:k]
 
     # ---- device-resident batch API (torch tensors already in HBM)
     def encode_batch_dev(self, d_in, offs: np.ndarray, p: Params, d_out, out_offs: np.ndarray, stream_ptr: int = 0):

@@ -72,6 +72,28 @@ def gather_streams(payload, lens: np.ndarray, dst: int = 0, group=None) -> Tuple
     return None, None, None
 
 
+def rank_streams(nstreams: int, rank: int, world: int) -> np.ndarray:
+    """Streams of `rank` when one buffer's independent streams are dealt round-robin
+    over `world` ranks (rank r takes {i : i mod G = r})."""
+    return np.arange(rank, nstreams, world, dtype=np.int64)
+
+
+def stream_order(counts: Sequence[int], world: int) -> np.ndarray:
+    """Global stream index of every gathered stream, for payloads gathered in rank
+    order (rank 0's streams, then rank 1's, ...) from a round-robin deal."""
+    idx = [rank_streams(int(sum(counts)), r, world)[:int(counts[r])] for r in range(world)]
+    return np.concatenate(idx) if idx else np.zeros(0, np.int64)
+
+
+def reorder_payloads(gathered: bytes, lens: Sequence[int], order: Sequence[int]) -> List[bytes]:
+    """Split a gathered buffer into its streams and put them back in global order."""
+    offs = np.concatenate([[0], np.cumsum(np.asarray(lens, dtype=np.int64))])
+    out: List[bytes] = [b""] * len(order)
+    for k, g in enumerate(order):
+        out[int(g)] = gathered[int(offs[k]):int(offs[k + 1])]
+    return out
+
+
 def _global(r: int, group) -> int:
     import torch.distributed as td
     if group is None:

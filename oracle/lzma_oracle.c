@@ -192,10 +192,17 @@ typedef struct {
     uint32_t min_match_check, direct_bytes;
     int hash_array;
     uint32_t *son, *hash;
+    uint64_t son_cap, hash_cap;   /* allocated entries (kept across streams by a session) */
 } bt_t;
 
+/* Create + Init. A session (oracle_enc_new) passes the previous stream's bt_t:
+ * like BinTree.Create (BinTree.java:108-133) the arrays are kept when they are
+ * large enough, and Init clears the hash heads (BinTree.java:72-80). */
 static int bt_create(bt_t *t, const uint8_t *buf, uint64_t n, uint32_t dict, uint32_t fb, int num_hash_bytes) {
+    uint32_t *old_son = t->son, *old_hash = t->hash;
+    uint64_t old_son_cap = t->son_cap, old_hash_cap = t->hash_cap;
     memset(t, 0, sizeof(*t));
+    t->son = old_son; t->hash = old_hash; t->son_cap = old_son_cap; t->hash_cap = old_hash_cap;
     t->buf = buf;
     /* SetType (BinTree.java:59-70) */
     t->hash_array = num_hash_bytes > 2;
@@ -220,9 +227,19 @@ static int bt_create(bt_t *t, const uint8_t *buf, uint64_t n, uint32_t dict, uin
         hs = (uint32_t)h + 1 + t->fix_hash_size;
     }
     t->hash_size_sum = hs;
-    t->son = (uint32_t *)calloc((size_t)t->cyc_size * 2, sizeof(uint32_t));
-    t->hash = (uint32_t *)calloc(hs, sizeof(uint32_t));
+    if (t->son_cap < (uint64_t)t->cyc_size * 2) {
+        free(t->son);
+        t->son = (uint32_t *)malloc((size_t)t->cyc_size * 2 * sizeof(uint32_t));
+        t->son_cap = t->son ? (uint64_t)t->cyc_size * 2 : 0;
+    }
+    if (t->hash_cap < hs) {
+        free(t->hash);
+        t->hash = (uint32_t *)malloc((size_t)hs * sizeof(uint32_t));
+        t->hash_cap = t->hash ? hs : 0;
+    }
     if (!t->son || !t->hash) return -1;
+    memset(t->son, 0, (size_t)t->cyc_size * 2 * sizeof(uint32_t));
+    memset(t->hash, 0, (size_t)hs * sizeof(uint32_t));   /* kEmptyHashValue, BinTree.java:76-77 */
     /* Init (BinTree.java:72-80 + InWindow.java:89-95): whole stream resident */
     t->base = -1;
     t->pos = 1;
@@ -230,7 +247,7 @@ static int bt_create(bt_t *t, const uint8_t *buf, uint64_t n, uint32_t dict, uin
     t->cyc_pos = 0;
     return 0;
 }
-static void bt_free(bt_t *t) { free(t->son); free(t->hash); t->son = t->hash = NULL; }
+static void bt_free(bt_t *t) { free(t->son); free(t->hash); t->son = t->hash = NULL; t->son_cap = t->hash_cap = 0; }
 
 static void bt_normalize(bt_t *t) {          /* BinTree.java:358-375 */
     uint32_t sub = t->pos - t->cyc_size;
@@ -927,8 +944,9 @@ static int enc_run(enc_t *e, const uint8_t *in, uint64_t n) {
     /* Create (Encoder.java:224-241) */
     if (bt_create(&e->bt, in, n, dict, e->num_fast_bytes, p->mf == 0 ? 2 : 4) != 0) return -2;
     size_t nlit = (size_t)1 << (e->lc + e->lp);
-    e->lit = (uint16_t *)malloc(nlit * 0x300 * sizeof(uint16_t));
+    if (!e->lit) e->lit = (uint16_t *)malloc(nlit * 0x300 * sizeof(uint16_t));
     if (!e->lit) return -2;
+    e->out.n = 0; e->out.oom = 0;
     /* Init (Encoder.java:247-273) */
     e->state = 0; e->previous_byte = 0;
     for (int i = 0; i < 4; i++) e->rep_distances[i] = 0;
@@ -1021,6 +1039,7 @@ int64_t oracle_match_lists(const uint8_t *in, uint64_t n, const oracle_params *p
     init_tables();
     if (check_params(p) != 0) return -1;
     bt_t t;
+    memset(&t, 0, sizeof t);
     if (bt_create(&t, in, n, (uint32_t)p->dict_size, (uint32_t)p->fb, p->mf == 0 ? 2 : 4) != 0) { bt_free(&t); return -1; }
     uint32_t l[kMatchMaxLen + 1], d[kMatchMaxLen + 1];
     uint64_t total = 0;
@@ -1080,6 +1099,46 @@ done:
 }
 
 void oracle_free(void *ptr) { free(ptr); }
+
+/* A session = one reused Encoder instance (one instance per
+ * thread, as a Java caller keeps one Encoder and calls Code per chunk). */
+struct oracle_enc { enc_t *e; };
+
+oracle_enc *oracle_enc_new(const oracle_params *p) {
+    init_tables();
+    if (check_params(p) != 0) return NULL;
+    oracle_enc *s = (oracle_enc *)calloc(1, sizeof(oracle_enc));
+    if (!s) return NULL;
+    s->e = (enc_t *)calloc(1, sizeof(enc_t));
+    if (!s->e) { free(s); return NULL; }
+    s->e->prm = *p;
+    return s;
+}
+
+int oracle_enc_code(oracle_enc *s, const uint8_t *in, uint64_t n, const uint8_t **out, uint64_t *out_len) {
+    enc_t *e = s->e;
+    /* reset the per-call state the way Encoder.Init/SetStreams do; keep the buffers */
+    bt_t bt = e->bt;
+    uint16_t *lit = e->lit;
+    obuf_t ob = e->out;
+    oracle_params prm = e->prm;
+    memset(e, 0, sizeof(*e));
+    e->bt = bt; e->lit = lit; e->out = ob; e->prm = prm;
+    int rc = enc_run(e, in, n);
+    if (rc != 0) return rc;
+    *out = e->out.p;
+    *out_len = e->out.n;
+    return 0;
+}
+
+void oracle_enc_delete(oracle_enc *s) {
+    if (!s) return;
+    free(s->e->out.p);
+    free(s->e->lit);
+    bt_free(&s->e->bt);
+    free(s->e);
+    free(s);
+}
 
 /* ============================================================ decoder */
 typedef struct {

@@ -44,6 +44,15 @@ int oracle_encode(const uint8_t *in, uint64_t n, const oracle_params *p, int mod
                   uint8_t **out, uint64_t *out_len);
 void oracle_free(void *ptr);
 
+/* Encoder session: one reused Encoder instance (its match-finder arrays are
+ * kept across calls and the hash heads cleared per call, BinTree.java:72-80,
+ * 108-133). oracle_enc_code's *out points into the session and stays valid
+ * until the next call. Same bytes as oracle_encode(mode 0). */
+typedef struct oracle_enc oracle_enc;
+oracle_enc *oracle_enc_new(const oracle_params *p);
+int oracle_enc_code(oracle_enc *s, const uint8_t *in, uint64_t n, const uint8_t **out, uint64_t *out_len);
+void oracle_enc_delete(oracle_enc *s);
+
 /* Decoder.SetDecoderProperties + Decoder.Code (Decoder.java:205-318).
  * out_size < 0 => decode until end marker. Returns 1 on success (Java true),
  * 0 on a corrupt stream (Java false), -1 on output overflow / bad props. */

@@ -47,6 +47,12 @@ def lib():
         L.oracle_rc_direct_bits.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
                                             ctypes.c_int]
         L.oracle_bittree_prices_after.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+        L.oracle_enc_new.argtypes = [ctypes.POINTER(Params)]
+        L.oracle_enc_new.restype = ctypes.c_void_p
+        L.oracle_enc_code.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                      ctypes.POINTER(ctypes.POINTER(ctypes.c_uint8)), ctypes.POINTER(ctypes.c_uint64)]
+        L.oracle_enc_code.restype = ctypes.c_int
+        L.oracle_enc_delete.argtypes = [ctypes.c_void_p]
         L.oracle_prob_price.argtypes = [ctypes.c_int]
         L.oracle_prob_price.restype = ctypes.c_uint32
         _lib = L
@@ -75,6 +81,35 @@ def encode(data, p=None, mode=0):
     res = ctypes.string_at(out, n.value)
     lib().oracle_free(out)
     return res
+
+
+class EncoderSession:
+    """One reused Encoder instance (oracle_enc_*): match-finder arrays kept
+    across calls, hash heads cleared per call as BinTree.Init does
+    (BinTree.java:72-80). Not thread-safe: one session per thread."""
+
+    def __init__(self, p):
+        self._p = p
+        self._h = lib().oracle_enc_new(ctypes.byref(p))
+        if not self._h:
+            raise RuntimeError("oracle_enc_new failed")
+
+    def encode(self, data):
+        a, ptr = _buf(data)
+        out = ctypes.POINTER(ctypes.c_uint8)()
+        n = ctypes.c_uint64()
+        rc = lib().oracle_enc_code(self._h, ptr, a.size, ctypes.byref(out), ctypes.byref(n))
+        if rc != 0:
+            raise RuntimeError("oracle_enc_code failed %d" % rc)
+        return ctypes.string_at(out, n.value)
+
+    def close(self):
+        if self._h:
+            lib().oracle_enc_delete(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
 
 
 def props(p):
@@ -115,3 +150,33 @@ def match_lists(data, p):
         if tot >= 0:
             return counts[:n], main[:n], lens[:tot], dists[:tot]
         cap *= 4
+
+
+def cpu_threads():
+    """Host threads for the oracle: the job's CPU share (OMP_NUM_THREADS on the GPU
+    box, else the affinity mask), at most 16."""
+    env = os.environ.get("OMP_NUM_THREADS")
+    n = int(env) if env and env.isdigit() else len(os.sched_getaffinity(0))
+    return max(1, min(n, 16))
+
+
+def encode_many(chunks, p, threads=None):
+    """Oracle encodings of independent chunks on a thread pool, one reused
+    EncoderSession per thread (ctypes releases the GIL inside the C calls)."""
+    import threading
+    from concurrent.futures import ThreadPoolExecutor
+    tl = threading.local()
+    sessions = []
+
+    def enc(c):
+        s = getattr(tl, "s", None)
+        if s is None:
+            s = tl.s = EncoderSession(p)
+            sessions.append(s)
+        return s.encode(c)
+
+    with ThreadPoolExecutor(max_workers=threads or cpu_threads()) as ex:
+        out = list(ex.map(enc, chunks))
+    for s in sessions:
+        s.close()
+    return out

@@ -215,3 +215,157 @@ def test_gpu_device_resident_api(ctx):
                                       (offs[1:] - offs[:-1]).astype(np.int64), d_dec, offs, st)
     assert (dst == 0).all()
     assert torch.equal(d_dec.cpu(), torch.from_numpy(data))
+
+
+# ---------------------------------------------------------------- match lists (SURVEY 7.1 instrumented mode)
+
+_MF_CASES = [
+    ("bench-L5", dict(dict_size=1 << 26, fb=32, mf=1), lambda: lzma_amd.bench_generate(200000).tobytes()),
+    ("text-d28", dict(dict_size=1 << 28, fb=32, mf=1), lambda: lzma_amd.text_generate(200000).tobytes()),
+    ("bt2-fb5", dict(dict_size=1 << 12, fb=5, mf=0), lambda: lzma_amd.bench_generate(100000).tobytes()),
+    ("small-dict", dict(dict_size=100, fb=64, mf=1), lambda: lzma_amd.text_generate(50000).tobytes()),
+    # alphabet of 4 with fb 273: most positions have far more than the 4 inline pairs,
+    # so the overflow pool (1 slot per 16 positions at first) must grow and retry
+    ("overflow-retry", dict(dict_size=1 << 20, fb=273, mf=1),
+     lambda: np.random.default_rng(3).integers(0, 4, 120000, dtype=np.uint8).tobytes()),
+]
+
+
+@pytest.mark.parametrize("name,kw,gen", _MF_CASES, ids=[c[0] for c in _MF_CASES])
+def test_gpu_match_lists_equal_oracle(ctx, name, kw, gen):
+    """mf.hip's per-position (len, dist) lists and extended main length against
+    BinTree.GetMatches at every position (oracle_match_lists), across several
+    streams of one batch (stream boundaries reset the window)."""
+    data = gen()
+    cuts = [0, len(data) // 3, len(data) // 3 + 7, len(data)]
+    streams = [data[cuts[i]:cuts[i + 1]] for i in range(len(cuts) - 1)]
+    p = lzma_amd.make_params(**kw)
+    counts, main, lens, dists = ctx.match_lists(streams, p)
+    g = 0
+    k = 0
+    for s in streams:
+        oc, om, ol, od = orc.match_lists(s, _oparams(p))
+        n = len(s)
+        assert np.array_equal(counts[g:g + n], oc), "counts differ"
+        assert np.array_equal(main[g:g + n], om), "main lengths differ"
+        t = int(oc.sum())
+        assert np.array_equal(lens[k:k + t], ol) and np.array_equal(dists[k:k + t], od), "pairs differ"
+        g += n
+        k += t
+    assert k == len(lens)
+    if name == "overflow-retry":
+        assert (counts > 4).mean() > 1 / 8   # the case really overflows the first pool
+
+
+def test_gpu_overflow_retry_encode_equals_oracle(ctx):
+    """The encoder consumes the regrown overflow pool: bytes equal Encoder.Code."""
+    data = np.random.default_rng(4).integers(0, 4, 150000, dtype=np.uint8).tobytes()
+    p = lzma_amd.make_params(dict_size=1 << 20, fb=273, mf=1)
+    fresh = lzma_amd.Context(0)   # no overflow-rate hint from earlier calls
+    try:
+        out = fresh.encode_batch([data, data[:70000]], p)
+    finally:
+        fresh.close()
+    assert out[0] == orc.encode(data, _oparams(p))
+    assert out[1] == orc.encode(data[:70000], _oparams(p))
+
+
+# ---------------------------------------------------------------- BASELINE.json configs at their own shapes
+
+def test_gpu_config1_rnd_1mib_lzma_alone_defaults(ctx):
+    """Config 1: 1 MiB of SplitMix64 bytes (seed 0x5EED) at LzmaAlone defaults
+    (d23 fb128 bt4 lc3 lp0 pb2): GPU bytes equal Encoder.Code's, and the round trip."""
+    data = lzma_amd.rnd_generate(1 << 20, 0x5EED).tobytes()
+    p = lzma_amd.make_params(dict_size=1 << 23, fb=128, mf=1)
+    blob = lzma_amd.compress_file_bytes(data, p, ctx)
+    assert blob == orc.lzma_file(data, _oparams(p))
+    assert lzma_amd.decompress_file_bytes(blob, ctx) == data
+
+
+def test_gpu_config2_shape_256_streams_l5_every_stream(ctx):
+    """Config 2's stream shape: 256 independent 256 KiB BENCH streams (64 MiB) at
+    dict 2^26 L5 (fb32 bt4 lc3 lp0 pb2), every stream byte-equal to the oracle."""
+    chunk = 256 << 10
+    data = lzma_amd.bench_generate(256 * chunk)
+    streams = [data[i:i + chunk] for i in range(0, data.size, chunk)]
+    p = lzma_amd.make_params(dict_size=1 << 26, fb=32, mf=1)
+    outs = ctx.encode_batch(streams, p)
+    ref = orc.encode_many([s.tobytes() for s in streams], _oparams(p))
+    bad = [i for i, (o, r) in enumerate(zip(outs, ref)) if o != r]
+    assert not bad, "streams differ: %s" % bad[:10]
+
+
+def test_gpu_config5_shape_4096_streams_dict18(ctx):
+    """Config 5: 4096 independent 256 KiB BENCH streams at dict 2^18 (1 GiB out).
+    GPU encode (a spread sample of 64 streams byte-equal to the oracle), GPU
+    decode of every stream back to the input, and GPU decode of the
+    oracle's own encodings of the sample."""
+    torch = pytest.importorskip("torch")
+    chunk, n = 256 << 10, 4096
+    data = lzma_amd.bench_generate(n * chunk)
+    p = lzma_amd.make_params(dict_size=1 << 18, fb=32, mf=1)
+    dev = torch.device("cuda", 0)
+    d_in = torch.from_numpy(data).to(dev)
+    offs = np.arange(n + 1, dtype=np.uint64) * np.uint64(chunk)
+    caps = np.array([lzma_amd.enc_bound(chunk)] * n, dtype=np.uint64)
+    cap_offs = np.zeros(n + 1, dtype=np.uint64)
+    cap_offs[1:] = np.cumsum(caps)
+    d_comp = torch.empty(int(cap_offs[-1]), dtype=torch.uint8, device=dev)
+    st = torch.cuda.current_stream(dev).cuda_stream
+    lens = ctx.encode_batch_dev(d_in, offs, p, d_comp, cap_offs, st)
+    d_pack = torch.empty(int(lens.sum()) + 1, dtype=torch.uint8, device=dev)
+    pk = ctx.pack_dev(d_comp, cap_offs, lens, d_pack, st)
+    host_pack = d_pack.cpu().numpy()
+    sample = list(range(0, n, n // 64))
+    ref = orc.encode_many([data[i * chunk:(i + 1) * chunk].tobytes() for i in sample], _oparams(p))
+    for i, r in zip(sample, ref):
+        assert host_pack[int(pk[i]):int(pk[i + 1])].tobytes() == r, "stream %d" % i
+    d_dec = torch.zeros(n * chunk, dtype=torch.uint8, device=dev)
+    dlens, dst = ctx.decode_batch_dev(lzma_amd.write_props(p), d_pack, pk, np.full(n, chunk, dtype=np.int64),
+                                      d_dec, offs, st)
+    assert (dst == 0).all() and (dlens == chunk).all()
+    assert torch.equal(d_dec, d_in)
+    res = ctx.decode_batch(ref, lzma_amd.write_props(p), [chunk] * len(ref))
+    for i, (s, d) in zip(sample, res):
+        assert s == lzma_amd.LZMA_OK and d == data[i * chunk:(i + 1) * chunk].tobytes()
+
+
+def test_gpu_config3_text_dict28(ctx):
+    """Config 3's parameters: TEXT input at dict 2^28 (hashMask 0x3FFFFFF: 26 hash
+    bits in the sort keys, distTableSize 56), L5, several 2 MiB streams, every
+    stream byte-equal to the oracle."""
+    chunk = 2 << 20
+    data = lzma_amd.text_generate(8 * chunk)
+    streams = [data[i:i + chunk].tobytes() for i in range(0, data.size, chunk)]
+    p = lzma_amd.make_params(dict_size=1 << 28, fb=32, mf=1)
+    outs = ctx.encode_batch(streams, p)
+    ref = orc.encode_many(streams, _oparams(p), threads=min(4, orc.cpu_threads()))
+    for i, (o, r) in enumerate(zip(outs, ref)):
+        assert o == r, "stream %d" % i
+    dec = ctx.decode_batch(outs, lzma_amd.write_props(p), [chunk] * len(outs))
+    for s, (st, d) in zip(streams, dec):
+        assert st == lzma_amd.LZMA_OK and d == s
+
+
+def test_gpu_single_stream_c_abi(ctx):
+    """lzma_encode / lzma_decode (the single-stream entry points a JNI shim binds
+    for Encoder.Code / Decoder.Code) through ctypes."""
+    import ctypes
+    L = lzma_amd.lib()
+    data = lzma_amd.text_generate(300000).tobytes()
+    p = lzma_amd.make_params(dict_size=1 << 22, fb=64, mf=1)
+    cap = lzma_amd.enc_bound(len(data))
+    out = (ctypes.c_uint8 * cap)()
+    n = ctypes.c_uint64()
+    assert L.lzma_encode(ctx.h, ctypes.byref(p), data, len(data), out, cap, ctypes.byref(n)) == lzma_amd.LZMA_OK
+    enc = bytes(out[:n.value])
+    assert enc == orc.encode(data, _oparams(p))
+    props = lzma_amd.write_props(p)
+    dec = (ctypes.c_uint8 * len(data))()
+    m = ctypes.c_uint64()
+    rc = L.lzma_decode(ctx.h, props, enc, len(enc), len(data), dec, len(data), ctypes.byref(m))
+    assert rc == lzma_amd.LZMA_OK and bytes(dec[:m.value]) == data
+    # too small an output buffer: LZMA_E_OVERFLOW, as the JNI decode loop expects
+    small = (ctypes.c_uint8 * 1000)()
+    rc = L.lzma_decode(ctx.h, props, enc, len(enc), -1, small, 1000, ctypes.byref(m))
+    assert rc == lzma_amd.LZMA_E_OVERFLOW
