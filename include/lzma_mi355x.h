@@ -17,6 +17,7 @@
  *   lzma_pack_dev         (framing) contiguous multi-stream container
  *   lzma_decode           Decoder.Code (one stream)          Decoder.java:205-301
  *   lzma_dec_batch[_dev]  Decoder.Code on N independent streams
+ *   lzma_*_batch_multi    the batch entry points over a device mask
  *   lzma_match_lists      BinTree.GetMatches at every position (diagnostic)  BinTree.java:152-273
  *   lzma_bench_generate   LzmaBench.CBenchRandomGenerator    LzmaBench.java:15-127
  *
@@ -111,6 +112,24 @@ int lzma_dec_batch(lzma_ctx *ctx, const uint8_t props[5],
                    uint64_t *out_lens, int32_t *status);
 int lzma_decode(lzma_ctx *ctx, const uint8_t props[5], const uint8_t *in, uint64_t n,
                 int64_t out_size, uint8_t *out, uint64_t out_cap, uint64_t *out_len);
+
+/* ---- several devices from one process (SURVEY 8(b) `device_mask`) --------
+ * A multi-device context holds one lzma_ctx per device whose bit is set in
+ * device_mask. The batch entry points deal the streams round-robin over those
+ * devices (the j-th selected device takes streams j, j+D, j+2D, ...: SURVEY
+ * 8(e)'s {i : i mod G = r}), run each device from its own host thread, and
+ * return the outputs in stream order, with the same layout and meaning as
+ * lzma_enc_batch / lzma_dec_batch. */
+typedef struct lzma_mctx lzma_mctx;
+int lzma_mctx_create(uint32_t device_mask, lzma_mctx **out);
+void lzma_mctx_destroy(lzma_mctx *m);
+const char *lzma_mctx_last_error(const lzma_mctx *m);
+int lzma_mctx_devices(const lzma_mctx *m);
+int lzma_enc_batch_multi(lzma_mctx *m, const lzma_params *p, const uint8_t *in, const uint64_t *offs, int nstreams,
+                         uint8_t *out, uint64_t out_cap, uint64_t *out_offs);
+int lzma_dec_batch_multi(lzma_mctx *m, const uint8_t props[5], const uint8_t *in, const uint64_t *in_offs,
+                         int nstreams, const int64_t *out_sizes, uint8_t *out, const uint64_t *out_offs,
+                         uint64_t *out_lens, int32_t *status);
 
 /* ---- instrumented mode --------------------------------------
  * The GPU match finder's per-position output for a batch of streams, as

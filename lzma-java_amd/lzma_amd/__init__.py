@@ -42,6 +42,8 @@ EXPORTED_SYMBOLS = [
     "lzma_pack_dev",
     "lzma_encode", "lzma_dec_batch_dev", "lzma_dec_batch", "lzma_decode", "lzma_bench_generate",
     "lzma_rnd_generate", "lzma_text_generate", "lzma_match_lists",
+    "lzma_mctx_create", "lzma_mctx_destroy", "lzma_mctx_last_error", "lzma_mctx_devices",
+    "lzma_enc_batch_multi", "lzma_dec_batch_multi",
 ]
 
 
@@ -105,6 +107,13 @@ def lib():
         L.lzma_decode.argtypes = [vp, vp, vp, u64, ctypes.c_int64, vp, u64, ctypes.POINTER(u64)]
         L.lzma_bench_generate.argtypes = [vp, u64]
         L.lzma_bench_generate.restype = None
+        L.lzma_mctx_create.argtypes = [ctypes.c_uint32, ctypes.POINTER(vp)]
+        L.lzma_mctx_destroy.argtypes = [vp]
+        L.lzma_mctx_last_error.argtypes = [vp]
+        L.lzma_mctx_last_error.restype = ctypes.c_char_p
+        L.lzma_mctx_devices.argtypes = [vp]
+        L.lzma_enc_batch_multi.argtypes = [vp, P, vp, vp, i32, vp, u64, vp]
+        L.lzma_dec_batch_multi.argtypes = [vp, vp, vp, vp, i32, vp, vp, vp, vp, vp]
         L.lzma_match_lists.argtypes = [vp, P, vp, vp, i32, vp, vp, vp, vp, u64, ctypes.POINTER(u64)]
         L.lzma_rnd_generate.argtypes = [vp, u64, u64]
         L.lzma_rnd_generate.restype = None
@@ -323,6 +332,61 @@ class Context:
                                             n, sizes.ctypes.data, _dptr(d_out), out_offs.ctypes.data,
                                             lens.ctypes.data, status.ctypes.data, ctypes.c_void_p(stream_ptr)))
         return lens[:n], status[:n]
+
+
+class MultiContext(Context):
+    """Several devices from one process (lzma_mctx, SURVEY 8(b) device_mask):
+    the batch calls deal the streams round-robin over the devices in the mask."""
+
+    def __init__(self, device_mask: int):
+        h = ctypes.c_void_p()
+        rc = lib().lzma_mctx_create(device_mask, ctypes.byref(h))
+        if rc != LZMA_OK:
+            raise LzmaError(rc, "lzma_mctx_create(mask=0x%x) failed" % device_mask)
+        self.h = h
+        self.device_mask = device_mask
+        self.devices = lib().lzma_mctx_devices(h)
+
+    def close(self):
+        if self.h:
+            lib().lzma_mctx_destroy(self.h)
+            self.h = None
+
+    def error(self) -> str:
+        return lib().lzma_mctx_last_error(self.h).decode()
+
+    def encode_batch(self, streams: Sequence[bytes], p: Params) -> List[bytes]:
+        arrs = [np.frombuffer(s, dtype=np.uint8) if not isinstance(s, np.ndarray) else s for s in streams]
+        offs = np.zeros(len(arrs) + 1, dtype=np.uint64)
+        np.cumsum([a.size for a in arrs], out=offs[1:])
+        data = np.concatenate(arrs) if arrs and offs[-1] > 0 else np.zeros(1, dtype=np.uint8)
+        cap = int(sum(enc_bound(a.size) for a in arrs)) + 1
+        out = np.empty(cap, dtype=np.uint8)
+        oo = np.zeros(len(arrs) + 1, dtype=np.uint64)
+        self.check(lib().lzma_enc_batch_multi(self.h, ctypes.byref(p), data.ctypes.data, offs.ctypes.data, len(arrs),
+                                              out.ctypes.data, cap, oo.ctypes.data))
+        return [out[oo[i]:oo[i + 1]].tobytes() for i in range(len(arrs))]
+
+    def decode_batch(self, streams: Sequence[bytes], props: bytes, out_sizes: Sequence[int],
+                     caps: Optional[Sequence[int]] = None) -> List[Tuple[int, bytes]]:
+        arrs = [np.frombuffer(s, dtype=np.uint8) for s in streams]
+        n = len(arrs)
+        io = np.zeros(n + 1, dtype=np.uint64)
+        np.cumsum([a.size for a in arrs], out=io[1:])
+        data = np.concatenate(arrs) if n and io[-1] > 0 else np.zeros(1, dtype=np.uint8)
+        if caps is None:
+            caps = [s if s >= 0 else max(64 * a.size, 4096) for s, a in zip(out_sizes, arrs)]
+        oo = np.zeros(n + 1, dtype=np.uint64)
+        np.cumsum(caps, out=oo[1:])
+        out = np.zeros(int(oo[-1]) + 1, dtype=np.uint8)
+        sizes = np.array(out_sizes, dtype=np.int64)
+        lens = np.zeros(max(n, 1), dtype=np.uint64)
+        status = np.zeros(max(n, 1), dtype=np.int32)
+        self.check(lib().lzma_dec_batch_multi(self.h, (ctypes.c_uint8 * 5)(*props[:5]), data.ctypes.data,
+                                              io.ctypes.data, n, sizes.ctypes.data, out.ctypes.data, oo.ctypes.data,
+                                              lens.ctypes.data, status.ctypes.data))
+        return [(int(status[i]), out[oo[i]:oo[i] + min(int(lens[i]), int(oo[i + 1] - oo[i]))].tobytes())
+                for i in range(n)]
 
 
 def _dptr(x) -> ctypes.c_void_p:

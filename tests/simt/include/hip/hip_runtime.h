@@ -19,6 +19,7 @@
 #include <barrier>
 #include <chrono>
 #include <functional>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -98,9 +99,9 @@ struct Sched {
     const std::function<void()>* body = nullptr;
     uint64_t xch[1024];
 };
-inline Sched g_sched;
-inline dim3 t_bid, g_bdim, g_gdim;
-inline dim3 g_dummy_tid;
+inline thread_local Sched g_sched;
+inline thread_local dim3 t_bid, g_bdim, g_gdim;
+inline thread_local dim3 g_dummy_tid;
 
 [[noreturn]] inline void fiber_entry() {
     Sched& s = g_sched;
@@ -128,7 +129,11 @@ inline void yield() {   // called on a fiber: back to the scheduler
 }
 inline void barrier() { yield(); }
 
+// one emulated kernel at a time process-wide: the LDS backing store (smem) is
+// shared, so host threads driving different emulated devices take turns
+inline std::mutex g_launch_mu;
 inline void launch(const std::function<void()>& body, dim3 grid, dim3 block) {
+    std::lock_guard<std::mutex> lk(g_launch_mu);
     const unsigned nt = block.x;
     g_bdim = block;
     g_gdim = grid;
@@ -241,8 +246,12 @@ inline unsigned atomicAdd(unsigned* p, unsigned v) { unsigned o = *p; *p = o + v
 inline unsigned long long atomicAdd(unsigned long long* p, unsigned long long v) { unsigned long long o = *p; *p = o + v; return o; }
 
 // ---- runtime API: device memory is host memory
-inline hipError_t hipGetDeviceCount(int* n) { *n = 1; return hipSuccess; }
-inline hipError_t hipSetDevice(int) { return hipSuccess; }
+inline hipError_t hipGetDeviceCount(int* n) {   // HIPEMU_DEVICES emulated devices (default 1)
+    const char* e = getenv("HIPEMU_DEVICES");
+    *n = e ? atoi(e) : 1;
+    return hipSuccess;
+}
+inline hipError_t hipSetDevice(int d) { int n = 0; hipGetDeviceCount(&n); return d >= 0 && d < n ? hipSuccess : 101; }
 inline hipError_t hipGetDevice(int* d) { *d = 0; return hipSuccess; }
 inline hipError_t hipDeviceGetAttribute(int* v, hipDeviceAttribute_t, int) { *v = 2; return hipSuccess; }
 inline hipError_t hipFuncSetAttribute(const void*, hipFuncAttribute, int) { return hipSuccess; }
