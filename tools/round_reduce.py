@@ -2,6 +2,8 @@
 
 stats   <dir> <out.csv>: per-kernel calls / total / mean duration (ms) with the
         dispatch's grid, LDS, VGPR and SGPR, from the kernel trace.
+counters <dir> <out.json> [workload-json]: per-kernel sum of every collected counter
+        per launch (e.g. the SQ_INSTS_* issue counters behind bench.py's roofline.issue).
 traffic <fetch_dir> <write_dir> <out.json>: per-kernel FETCH_SIZE and WRITE_SIZE
         per launch in bytes. rocprofv3 reports both in KiB; on gfx950 FETCH_SIZE
         counts 64 B per memory-side read request while wide streaming reads
@@ -54,7 +56,7 @@ def stats(d, out):
     print(open(out).read())
 
 
-def traffic(fd, wd, out):
+def traffic(fd, wd, out, workload=None):
     res = {}
     for d, cname in ((fd, "FETCH_SIZE"), (wd, "WRITE_SIZE")):
         per = collections.defaultdict(float)
@@ -76,8 +78,25 @@ def traffic(fd, wd, out):
         w = e.get("write_size_bytes_per_launch", 0.0)
         e["traffic_bytes_per_launch_raw"] = f + w
         e["traffic_bytes_per_launch"] = 2 * f + w
-    res["_workload"] = {"bytes_per_gpu": 1 << 30, "chunk": 256 << 10,
-                        "command": "bench.py --steps 1 --warmup 0 --cpu-sample 0 --no-verify"}
+    res["_workload"] = json.loads(workload) if workload else {
+        "bytes_per_gpu": 1 << 30, "chunk": 256 << 10, "data": "bench", "dict_log": 26,
+        "command": "bench.py --steps 1 --warmup 0 --cpu-sample 0 --no-verify"}
+    json.dump(res, open(out, "w"), indent=1, sort_keys=True)
+    print(json.dumps(res, indent=1, sort_keys=True))
+
+
+def counters(d, out, workload=None):
+    per = collections.defaultdict(lambda: collections.defaultdict(float))
+    disp = collections.defaultdict(set)
+    for r in rows(d, "counter_collection.csv"):
+        k = short(r["Kernel_Name"])
+        per[k][r["Counter_Name"]] += float(r["Counter_Value"])
+        disp[k].add(r["Dispatch_Id"])
+    res = {k: dict({c: v / max(len(disp[k]), 1) for c, v in cs.items()}, launches=len(disp[k]))
+           for k, cs in per.items()}
+    res["_workload"] = json.loads(workload) if workload else {}
+    res["_cus"] = 256
+    res["_sclk_hz"] = 2.4e9
     json.dump(res, open(out, "w"), indent=1, sort_keys=True)
     print(json.dumps(res, indent=1, sort_keys=True))
 
@@ -85,5 +104,7 @@ def traffic(fd, wd, out):
 if __name__ == "__main__":
     if sys.argv[1] == "stats":
         stats(sys.argv[2], sys.argv[3])
+    elif sys.argv[1] == "counters":
+        counters(sys.argv[2], sys.argv[3], sys.argv[4] if len(sys.argv) > 4 else None)
     else:
-        traffic(sys.argv[2], sys.argv[3], sys.argv[4])
+        traffic(sys.argv[2], sys.argv[3], sys.argv[4], sys.argv[5] if len(sys.argv) > 5 else None)
