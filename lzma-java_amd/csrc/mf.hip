@@ -137,6 +137,64 @@ __device__ inline uint64_t load8(const uint8_t* p) {
     return sh ? (lo >> sh) | (hi << (64 - sh)) : lo;
 }
 
+// First index r in [from, limit) with a[r] != b[r] (limit if none); when r < limit,
+// *a_less = a[r] < b[r]. 16 bytes per iteration: both sides' words are loaded in
+// one round trip, and the mismatching bytes come out of the loaded words (no
+// separate byte loads for the tree-walk direction).
+__device__ inline uint32_t cmp_run(const uint8_t* a, const uint8_t* b, uint32_t from, uint32_t limit, bool* a_less) {
+    uint32_t len = from;
+    while (len < limit) {
+        const uint64_t a0 = load8(a + len), b0 = load8(b + len);
+        const uint64_t a1 = load8(a + len + 8), b1 = load8(b + len + 8);
+        uint64_t xa = a0, x = a0 ^ b0, xb = b0;
+        uint32_t at = len;
+        if (!x) { xa = a1; xb = b1; x = a1 ^ b1; at = len + 8; }
+        if (x) {
+            const uint32_t sh = (uint32_t)__builtin_ctzll(x) & ~7u;
+            const uint32_t r = at + (sh >> 3);
+            if (r >= limit) return limit;
+            *a_less = ((xa >> sh) & 0xFFu) < ((xb >> sh) & 0xFFu);
+            return r;
+        }
+        len += 16;
+    }
+    return limit;
+}
+
+// One binary-tree node of the walk, by sorted bucket index: the two links of
+// BinTree._son (s0 = son[2i], s1 = son[2i + 1]; (1-based local position << 32) |
+// (sorted index + 1), 0 = none) and the first 16 bytes of the member's suffix.
+// A tree step loads one node (32 bytes, one request): its bytes for the compare
+// and its links for the descent -- the walk reads the stream's bytes only for
+// matches longer than 16.
+struct alignas(32) WNode {
+    uint64_t s0, s1, p0, p1;
+};
+
+// First index r in [from, min(16, limit)) where the 16-byte prefixes differ
+// (cur = c0|c1, candidate = q0|q1); 16 if they agree through byte 15 (the
+// caller continues in the stream); limit if r would reach it. *q_less = the
+// candidate's byte < the current byte at r.
+__device__ inline uint32_t pfx_cmp(uint64_t c0, uint64_t c1, uint64_t q0, uint64_t q1, uint32_t from, uint32_t limit,
+                                   bool* q_less) {
+    uint64_t xm, qa, ca;
+    uint32_t at;
+    if (from < 8) {
+        xm = (c0 ^ q0) & (~0ull << (8 * from));
+        qa = q0; ca = c0; at = 0;
+        if (!xm) { xm = c1 ^ q1; qa = q1; ca = c1; at = 8; }
+    } else {
+        xm = (c1 ^ q1) & (~0ull << (8 * (from - 8)));
+        qa = q1; ca = c1; at = 8;
+    }
+    if (!xm) return limit < 16 ? limit : 16;
+    const uint32_t sh = (uint32_t)__builtin_ctzll(xm) & ~7u;
+    const uint32_t r = at + (sh >> 3);
+    if (r >= limit) return limit;
+    *q_less = ((qa >> sh) & 0xFFu) < ((ca >> sh) & 0xFFu);
+    return r;
+}
+
 // Common-prefix length of a[0..limit) and b[0..limit), starting at `from`.
 __device__ inline uint32_t common_len(const uint8_t* a, const uint8_t* b, uint32_t from, uint32_t limit) {
     uint32_t len = from;
@@ -158,7 +216,7 @@ __global__ void __launch_bounds__(64) mf_walk_kernel(const uint8_t* __restrict__
                                                      const uint32_t* __restrict__ chain_start,
                                                      const uint32_t* __restrict__ chain_len,
                                                      const uint64_t* __restrict__ nchains_p,
-                                                     MfArgs a, uint32_t* __restrict__ son, PairT* __restrict__ pairs,
+                                                     MfArgs a, WNode* __restrict__ nodes, PairT* __restrict__ pairs,
                                                      uint32_t* __restrict__ ovf_off, PairT* __restrict__ ovf,
                                                      unsigned long long* __restrict__ ovf_used, uint64_t ovf_cap,
                                                      uint32_t ovf_stride,
@@ -181,10 +239,9 @@ __global__ void __launch_bounds__(64) mf_walk_kernel(const uint8_t* __restrict__
     const uint32_t fb = a.fb, cut = a.cut_value;
     const uint64_t cyc = a.cyc_size;
     uint32_t prev_local = 0;                // 1-based local position of previous bucket member, 0 = none
-    // son[] is indexed by the member's index in the sorted key array (not by
-    // position): a bucket's tree links then live in one contiguous run
-    // [2 start, 2 end), so a walk touches a few cache lines instead of one
-    // random line per step. Links hold sorted index + 1 (0 = no node).
+    // The tree nodes are indexed by the member's index in the sorted key array (not
+    // by position): a bucket's tree lives in one contiguous run of WNodes, so a
+    // walk touches a few cache lines instead of one random line per step.
     for (uint64_t i = start; i < end; i++) {
         uint64_t g = vals4[i];
         uint32_t p = (uint32_t)(g - base);
@@ -222,13 +279,15 @@ __global__ void __launch_bounds__(64) mf_walk_kernel(const uint8_t* __restrict__
             last_d = d;
             cnt++;
         };
+        const uint64_t c0 = load8(cur), c1 = load8(cur + 8);   // this member's prefix
+        const uint32_t cur0 = (uint32_t)(c0 & 0xFFu);
         if (BT4) {   // hash2 / hash3 candidates, BinTree.java:183-207
             uint32_t pv2 = __builtin_nontemporal_load(a.prev2 + g), pv3 = __builtin_nontemporal_load(a.prev3 + g);
             uint32_t cm2 = pv2 == kNoPos ? 0 : (uint32_t)(pv2 - base) + 1;
             uint32_t cm3 = pv3 == kNoPos ? 0 : (uint32_t)(pv3 - base) + 1;
-            if (cm2 > match_min && sb[cm2 - 1] == cur[0]) { max_len = 2; emit(2, pos - cm2 - 1); }
+            if (cm2 > match_min && sb[cm2 - 1] == cur0) { max_len = 2; emit(2, pos - cm2 - 1); }
             const uint32_t d2 = pos - cm2 - 1;   // the len-2 pair's distance, if it was emitted
-            if (cm3 > match_min && sb[cm3 - 1] == cur[0]) {
+            if (cm3 > match_min && sb[cm3 - 1] == cur0) {
                 if (cm3 == cm2) cnt--;
                 max_len = 3;
                 emit(3, pos - cm3 - 1);
@@ -240,7 +299,10 @@ __global__ void __launch_bounds__(64) mf_walk_kernel(const uint8_t* __restrict__
                 if (cnt == 1) { last_l = 2; last_d = d2; }   // the len-2 pair is the last one again
             }
         }
-        uint64_t ptr0 = 2 * i + 1, ptr1 = 2 * i;
+        nodes[i].p0 = c0;
+        nodes[i].p1 = c1;
+        uint64_t* ptr0 = &nodes[i].s1;      // BinTree ptr0 = son[2i + 1], ptr1 = son[2i]
+        uint64_t* ptr1 = &nodes[i].s0;
         uint64_t cur_idx = i - 1;           // sorted index of the head (valid while cur_match != 0)
         uint32_t len0 = a.direct_bytes, len1 = a.direct_bytes;
         if (!BT4 && cur_match > match_min) {   // BT2 direct byte check, BinTree.java:218-226
@@ -248,24 +310,29 @@ __global__ void __launch_bounds__(64) mf_walk_kernel(const uint8_t* __restrict__
         }
         uint32_t count = cut;
         for (;;) {   // BinTree.java:230-270
-            if (cur_match <= match_min || count-- == 0) { son[ptr0] = 0; son[ptr1] = 0; break; }
+            if (cur_match <= match_min || count-- == 0) { *ptr0 = 0; *ptr1 = 0; break; }
             uint32_t delta = pos - cur_match;
-            uint64_t cp = 2 * cur_idx;
-            const uint8_t* pby = sb + (cur_match - 1);
+            const WNode nd = nodes[cur_idx];
             uint32_t len = len0 < len1 ? len0 : len1;
-            if (pby[len] == cur[len]) {
-                len = common_len(pby, cur, len + 1, len_limit);
+            // BinTree.java:243-248: the bytes equal at len => extend; the direction
+            // (:259) compares the bytes at the first mismatch
+            bool pby_less = false;
+            uint32_t l2 = len < 16 ? pfx_cmp(c0, c1, nd.p0, nd.p1, len, len_limit, &pby_less) : len;
+            if (l2 >= 16 && l2 < len_limit) l2 = cmp_run(sb + (cur_match - 1), cur, l2, len_limit, &pby_less);
+            if (l2 > len) {
+                len = l2;
                 if (max_len < len) {
                     max_len = len;
                     emit(len, delta - 1);
-                    if (len == len_limit) { son[ptr1] = son[cp]; son[ptr0] = son[cp + 1]; break; }
+                    if (len == len_limit) { *ptr1 = nd.s0; *ptr0 = nd.s1; break; }
                 }
             }
-            uint32_t nxt;
-            if (pby[len] < cur[len]) { son[ptr1] = (uint32_t)(cur_idx + 1); ptr1 = cp + 1; nxt = son[ptr1]; len1 = len; }
-            else { son[ptr0] = (uint32_t)(cur_idx + 1); ptr0 = cp; nxt = son[ptr0]; len0 = len; }
+            const uint64_t node = ((uint64_t)cur_match << 32) | (uint32_t)(cur_idx + 1);
+            uint64_t nxt;
+            if (pby_less) { *ptr1 = node; ptr1 = &nodes[cur_idx].s1; nxt = nd.s1; len1 = len; }
+            else { *ptr0 = node; ptr0 = &nodes[cur_idx].s0; nxt = nd.s0; len0 = len; }
             if (nxt == 0) cur_match = 0;
-            else { cur_idx = nxt - 1; cur_match = (uint32_t)(vals4[cur_idx] - base) + 1; }
+            else { cur_idx = (uint32_t)nxt - 1; cur_match = (uint32_t)(nxt >> 32); }
         }
         uint32_t ml = 0;
         if (cnt > 0) {   // Encoder.ReadMatchDistances extension, Encoder.java:279-284
@@ -402,12 +469,14 @@ int run_match_finder(Ctx* ctx, const Derived& d, const uint8_t* in, const uint64
         const unsigned WB = 64;
         unsigned grid = (unsigned)((nchains + WB - 1) / WB);
         grid = (grid + 7) & ~7u;   // multiple of 8 (XCD-aware mapping in mf_walk_kernel)
+        // experiment: dynamic LDS per wave caps the waves per CU (L2 working set)
+        static const size_t walk_lds = getenv("LZG_WALK_LDS") ? (size_t)atoi(getenv("LZG_WALK_LDS")) : 0;
         if (wide_pairs) {
-            if (bt4) hipLaunchKernelGGL((mf_walk_kernel<uint64_t, true>), dim3(grid), dim3(WB), 0, st, in, d_offs, w.ks, w.vs, w.chain_order, w.chain_start, w.chain_len, w.counts + 1, a, w.son, (uint64_t*)w.pairs, w.ovf_off, (uint64_t*)w.ovf, w.ovf_used, w.ovf_cap, ovf_stride(d.fb), w.err);
-            else hipLaunchKernelGGL((mf_walk_kernel<uint64_t, false>), dim3(grid), dim3(WB), 0, st, in, d_offs, w.ks, w.vs, w.chain_order, w.chain_start, w.chain_len, w.counts + 1, a, w.son, (uint64_t*)w.pairs, w.ovf_off, (uint64_t*)w.ovf, w.ovf_used, w.ovf_cap, ovf_stride(d.fb), w.err);
+            if (bt4) hipLaunchKernelGGL((mf_walk_kernel<uint64_t, true>), dim3(grid), dim3(WB), walk_lds, st, in, d_offs, w.ks, w.vs, w.chain_order, w.chain_start, w.chain_len, w.counts + 1, a, (WNode*)w.son, (uint64_t*)w.pairs, w.ovf_off, (uint64_t*)w.ovf, w.ovf_used, w.ovf_cap, ovf_stride(d.fb), w.err);
+            else hipLaunchKernelGGL((mf_walk_kernel<uint64_t, false>), dim3(grid), dim3(WB), walk_lds, st, in, d_offs, w.ks, w.vs, w.chain_order, w.chain_start, w.chain_len, w.counts + 1, a, (WNode*)w.son, (uint64_t*)w.pairs, w.ovf_off, (uint64_t*)w.ovf, w.ovf_used, w.ovf_cap, ovf_stride(d.fb), w.err);
         } else {
-            if (bt4) hipLaunchKernelGGL((mf_walk_kernel<uint32_t, true>), dim3(grid), dim3(WB), 0, st, in, d_offs, w.ks, w.vs, w.chain_order, w.chain_start, w.chain_len, w.counts + 1, a, w.son, (uint32_t*)w.pairs, w.ovf_off, (uint32_t*)w.ovf, w.ovf_used, w.ovf_cap, ovf_stride(d.fb), w.err);
-            else hipLaunchKernelGGL((mf_walk_kernel<uint32_t, false>), dim3(grid), dim3(WB), 0, st, in, d_offs, w.ks, w.vs, w.chain_order, w.chain_start, w.chain_len, w.counts + 1, a, w.son, (uint32_t*)w.pairs, w.ovf_off, (uint32_t*)w.ovf, w.ovf_used, w.ovf_cap, ovf_stride(d.fb), w.err);
+            if (bt4) hipLaunchKernelGGL((mf_walk_kernel<uint32_t, true>), dim3(grid), dim3(WB), walk_lds, st, in, d_offs, w.ks, w.vs, w.chain_order, w.chain_start, w.chain_len, w.counts + 1, a, (WNode*)w.son, (uint32_t*)w.pairs, w.ovf_off, (uint32_t*)w.ovf, w.ovf_used, w.ovf_cap, ovf_stride(d.fb), w.err);
+            else hipLaunchKernelGGL((mf_walk_kernel<uint32_t, false>), dim3(grid), dim3(WB), walk_lds, st, in, d_offs, w.ks, w.vs, w.chain_order, w.chain_start, w.chain_len, w.counts + 1, a, (WNode*)w.son, (uint32_t*)w.pairs, w.ovf_off, (uint32_t*)w.ovf, w.ovf_used, w.ovf_cap, ovf_stride(d.fb), w.err);
         }
     }
     LZG_TRACE(ctx, st, "mf_walk done (%llu chains)", (unsigned long long)nchains);

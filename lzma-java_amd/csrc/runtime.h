@@ -35,7 +35,7 @@ struct MfBuffers {
     uint8_t* flag;
     uint32_t *chain_start, *chain_len, *chain_len_sorted, *chain_idx, *chain_order;
     uint64_t* counts;
-    uint32_t* son;
+    uint64_t* son;                // walk tree nodes (mf.hip WNode, 32 B per position: links + 16-byte prefix)
     void* pairs;
     uint32_t* ovf_off;
     void* ovf;

@@ -144,7 +144,7 @@ static int encode_pass(Ctx* ctx, const Derived& d, const uint8_t* d_in, const ui
             w.chain_start = c.take<uint32_t>(T); w.chain_len = c.take<uint32_t>(T); w.chain_len_sorted = c.take<uint32_t>(T);
             w.chain_idx = c.take<uint32_t>(T); w.chain_order = c.take<uint32_t>(T);
             w.counts = c.take<uint64_t>(2);
-            w.son = c.take<uint32_t>(2 * T);
+            w.son = c.take<uint64_t>(4 * T);   // mf.hip WNode: 32 bytes per position
             w.pairs = c.take<uint8_t>(T * kInlinePairs * psz);
             w.ovf_off = c.take<uint32_t>(T);
             w.ovf = c.take<uint8_t>(ovf_cap * psz);

@@ -27,11 +27,13 @@ def main():
     ap.add_argument("--parity", type=int, default=8)
     ap.add_argument("--size", type=int, default=1 << 30)
     ap.add_argument("--chunk", type=int, default=256 << 10)
+    ap.add_argument("--data", choices=["bench", "text"], default="bench")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(0)
     st = torch.cuda.current_stream(dev).cuda_stream
-    host = lzma_amd.bench_generate(args.size)
+    host = lzma_amd.generate(args.data, args.size)
+    dict_log = 28 if args.data == "text" else 26
     n = args.size // args.chunk
     offs = np.arange(n + 1, dtype=np.uint64) * np.uint64(args.chunk)
     cap_offs = np.zeros(n + 1, dtype=np.uint64)
@@ -40,12 +42,12 @@ def main():
     d_comp = torch.empty(int(cap_offs[-1]), dtype=torch.uint8, device=dev)
     d_pack = torch.empty(int(cap_offs[-1]), dtype=torch.uint8, device=dev)
     d_dec = torch.empty(args.size, dtype=torch.uint8, device=dev)
-    p = lzma_amd.make_params(dict_size=1 << 26, fb=32, mf=1, lc=3, lp=0, pb=2)
+    p = lzma_amd.make_params(dict_size=1 << dict_log, fb=32, mf=1, lc=3, lp=0, pb=2)
     props = lzma_amd.write_props(p)
     ctx, cdec = lzma_amd.Context(0), lzma_amd.Context(0)
     ctx.set_batch_bytes(1 << 30)
     sizes = np.full(n, args.chunk, dtype=np.int64)
-    res = {"lib": os.environ.get("LZMA_AMD_LIB", "product")}
+    res = {"lib": os.environ.get("LZMA_AMD_LIB", "product"), "data": args.data}
     walls = []
     for rep in range(args.reps + 1):
         if rep == 1:
@@ -71,12 +73,12 @@ def main():
         idx = np.linspace(0, n - 1, args.parity).astype(int)
         hp = d_pack[:int(pk[-1])].cpu().numpy()
         ref = orc.encode_many([host[int(offs[i]):int(offs[i + 1])].tobytes() for i in idx],
-                              orc.params(1 << 26, 32, 1, 3, 0, 2, 0))
+                              orc.params(1 << dict_log, 32, 1, 3, 0, 2, 0))
         par = all(hp[int(pk[i]):int(pk[i + 1])].tobytes() == r for i, r in zip(idx, ref))
     enc_s = min(w[0] for w in walls)
     dec_s = min(w[1] for w in walls)
     res.update(enc_s=enc_s, dec_s=dec_s, MBps=args.size / (enc_s + dec_s) / 1e6,
-               kernels_ms={k: round(v[0] / max(v[1], 1) * (v[1] / args.reps), 2) for k, v in tm.items()},
+               kernels_ms={k: round(v[0] / args.reps, 2) for k, v in tm.items()},
                roundtrip=ok, parity=par, ratio=float(lens.sum()) / args.size)
     print(json.dumps(res), flush=True)
 
