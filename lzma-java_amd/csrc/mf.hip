@@ -242,8 +242,15 @@ __global__ void __launch_bounds__(64) mf_walk_kernel(const uint8_t* __restrict__
     // The tree nodes are indexed by the member's index in the sorted key array (not
     // by position): a bucket's tree lives in one contiguous run of WNodes, so a
     // walk touches a few cache lines instead of one random line per step.
+    // Memory ordering matters here: on CDNA a load's wait also waits for every
+    // store issued before it, so each step issues the next node's load before
+    // its own link store, the pairs of a position stay in registers until the
+    // position ends, and the newest member's node (the next position's first
+    // tree node) is carried in registers instead of being re-read.
+    WNode head{};                            // node of the previous member (valid when prev_local != 0)
+    uint64_t g = vals4[start];
     for (uint64_t i = start; i < end; i++) {
-        uint64_t g = vals4[i];
+        const uint64_t g_next = i + 1 < end ? vals4[i + 1] : 0;
         uint32_t p = (uint32_t)(g - base);
         uint32_t pos = p + 1;               // BinTree 1-based position
         uint64_t rem = n - p;
@@ -252,17 +259,16 @@ __global__ void __launch_bounds__(64) mf_walk_kernel(const uint8_t* __restrict__
         const uint8_t* cur = sb + p;
         uint32_t cur_match = prev_local;
         uint32_t max_len = 1, cnt = 0;
-        PairT* inl = pairs + g * kInlinePairs;
+        PairT q0 = 0, q1 = 0, q2 = 0, q3 = 0;   // the inline pairs, stored when the position ends
         PairT* ov = nullptr;
         bool ov_ok = false;
         // the last emitted pair stays in registers: the fb extension below must not
         // re-read it from memory (a failed overflow allocation leaves no copy there)
         uint32_t last_l = 0, last_d = 0;
         auto emit = [&](uint32_t l, uint32_t d) {
+            const PairT v = PP::pack(l, d);
             if (cnt < kInlinePairs) {
-                // outputs and the hash2/3 links are touched once: non-temporal, so the
-                // stream's tree links and bytes keep the L2
-                __builtin_nontemporal_store(PP::pack(l, d), inl + cnt);
+                q0 = cnt == 0 ? v : q0; q1 = cnt == 1 ? v : q1; q2 = cnt == 2 ? v : q2; q3 = cnt == 3 ? v : q3;
             } else {
                 if (ov == nullptr) {
                     // the pool is handed out in slots of ovf_stride pairs: a position
@@ -273,7 +279,7 @@ __global__ void __launch_bounds__(64) mf_walk_kernel(const uint8_t* __restrict__
                     ovf_off[g] = (uint32_t)o;
                     ov = ovf + o * ovf_stride;
                 }
-                if (ov_ok) ov[cnt - kInlinePairs] = PP::pack(l, d);
+                if (ov_ok) ov[cnt - kInlinePairs] = v;
             }
             last_l = l;
             last_d = d;
@@ -299,38 +305,46 @@ __global__ void __launch_bounds__(64) mf_walk_kernel(const uint8_t* __restrict__
                 if (cnt == 1) { last_l = 2; last_d = d2; }   // the len-2 pair is the last one again
             }
         }
-        nodes[i].p0 = c0;
-        nodes[i].p1 = c1;
-        uint64_t* ptr0 = &nodes[i].s1;      // BinTree ptr0 = son[2i + 1], ptr1 = son[2i]
+        // this member's node: its links are set by its own walk (tracked in registers
+        // while ptr0/ptr1 still point at it), its prefix is c0|c1
+        WNode self{0, 0, c0, c1};
+        bool p0_self = true, p1_self = true;   // ptr0 = son[2i + 1] (s1), ptr1 = son[2i] (s0)
+        uint64_t* ptr0 = &nodes[i].s1;
         uint64_t* ptr1 = &nodes[i].s0;
+        auto put0 = [&](uint64_t v) { if (p0_self) self.s1 = v; else *ptr0 = v; };
+        auto put1 = [&](uint64_t v) { if (p1_self) self.s0 = v; else *ptr1 = v; };
         uint64_t cur_idx = i - 1;           // sorted index of the head (valid while cur_match != 0)
         uint32_t len0 = a.direct_bytes, len1 = a.direct_bytes;
         if (!BT4 && cur_match > match_min) {   // BT2 direct byte check, BinTree.java:218-226
             if (sb[cur_match - 1 + 2] != cur[2]) { max_len = 2; emit(2, pos - cur_match - 1); }
         }
+        WNode nd = head;                    // the first node visited is the previous member
         uint32_t count = cut;
         for (;;) {   // BinTree.java:230-270
-            if (cur_match <= match_min || count-- == 0) { *ptr0 = 0; *ptr1 = 0; break; }
+            if (cur_match <= match_min || count-- == 0) { put0(0); put1(0); break; }
             uint32_t delta = pos - cur_match;
-            const WNode nd = nodes[cur_idx];
             uint32_t len = len0 < len1 ? len0 : len1;
             // BinTree.java:243-248: the bytes equal at len => extend; the direction
             // (:259) compares the bytes at the first mismatch
             bool pby_less = false;
             uint32_t l2 = len < 16 ? pfx_cmp(c0, c1, nd.p0, nd.p1, len, len_limit, &pby_less) : len;
             if (l2 >= 16 && l2 < len_limit) l2 = cmp_run(sb + (cur_match - 1), cur, l2, len_limit, &pby_less);
+            bool emit_now = false;
             if (l2 > len) {
                 len = l2;
                 if (max_len < len) {
                     max_len = len;
-                    emit(len, delta - 1);
-                    if (len == len_limit) { *ptr1 = nd.s0; *ptr0 = nd.s1; break; }
+                    if (len == len_limit) { emit(len, delta - 1); put1(nd.s0); put0(nd.s1); break; }
+                    emit_now = true;
                 }
             }
             const uint64_t node = ((uint64_t)cur_match << 32) | (uint32_t)(cur_idx + 1);
-            uint64_t nxt;
-            if (pby_less) { *ptr1 = node; ptr1 = &nodes[cur_idx].s1; nxt = nd.s1; len1 = len; }
-            else { *ptr0 = node; ptr0 = &nodes[cur_idx].s0; nxt = nd.s0; len0 = len; }
+            const uint64_t nxt = pby_less ? nd.s1 : nd.s0;
+            uint64_t* const here = pby_less ? &nodes[cur_idx].s1 : &nodes[cur_idx].s0;
+            if (nxt != 0) nd = nodes[(uint32_t)nxt - 1];   // issued before this step's stores
+            if (pby_less) { put1(node); ptr1 = here; p1_self = false; len1 = len; }
+            else { put0(node); ptr0 = here; p0_self = false; len0 = len; }
+            if (emit_now) emit(len, delta - 1);
             if (nxt == 0) cur_match = 0;
             else { cur_idx = (uint32_t)nxt - 1; cur_match = (uint32_t)(nxt >> 32); }
         }
@@ -345,8 +359,17 @@ __global__ void __launch_bounds__(64) mf_walk_kernel(const uint8_t* __restrict__
                 ml += common_len(sb + from - d1, sb + from, 0, (uint32_t)lim);
             }
         }
+        nodes[i] = self;
+        head = self;
+        // outputs are touched once: non-temporal, so the stream's nodes and bytes keep the L2
+        PairT* inl = pairs + g * kInlinePairs;
+        __builtin_nontemporal_store(q0, inl + 0);
+        __builtin_nontemporal_store(q1, inl + 1);
+        __builtin_nontemporal_store(q2, inl + 2);
+        __builtin_nontemporal_store(q3, inl + 3);
         __builtin_nontemporal_store(cnt | (ml << 16), a.minfo + g);
         prev_local = pos;
+        g = g_next;
     }
 }
 
