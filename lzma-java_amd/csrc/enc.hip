@@ -42,7 +42,7 @@ constexpr int kRing = 32;           // match-info prefetch window (positions)
 constexpr int kGW = 64;             // gather window: offsets -1 .. kGW-2 around the current position
 constexpr int kGI = kGW / kWave;    // gather iterations per side (1 on hardware)
 constexpr int kSides = 7;           // cur, rep0..rep3, pair0, pair1
-constexpr int kObuf = 256;          // output staging ring (bytes, power of two)
+constexpr int kRbuf = 128;          // coder-record staging ring (records, power of two; halves of 64 go to HBM)
 constexpr int kLitSlots = (8 + kWave - 1) / kWave;   // literal bits per lane (1 on hardware)
 static_assert(kSides * kGW >= kNumFullDistances * 2, "tempPrices alias the gather window");
 
@@ -151,7 +151,7 @@ struct Enc {
     uint32_t* o_bytes;        // [kOptLds] cur byte | match byte << 8 | previous byte << 16 of each parsed
                               // position, so the coder needs no HBM byte loads
     uint8_t* win;             // gather window [kSides][kGW]: cur side, reps 0-3, pairs 0-1
-    uint8_t* obuf;            // output staging ring [kObuf]
+    uint16_t* rbuf;           // coder-record staging ring [kRbuf]
     __amdgpu_buffer_rsrc_t spill;   // _optimum slots >= kOptLds in HBM (9 fields x kNumOpts dwords)
     // ---- parameters
     uint32_t fb, lc, lp, pb, ps_mask, eos, dist_table_size, tsize;
@@ -162,8 +162,8 @@ struct Enc {
     uint32_t bad;                 // internal-consistency watchdog tripped (reason code, 0 = fine)
     uint32_t wd, wd_max;          // loop-iteration watchdog (budget per stream)
     uint32_t* dbg;
-    uint8_t* out;
-    uint32_t cap, outpos;      // streams < 2 GiB: outputs < 4 GiB
+    uint16_t* recs;           // the stream's coder records in HBM (rc.hip codes them)
+    uint64_t rcap, rpos;      // record capacity / records emitted
     uint32_t overflow;
     const uint32_t* minfo;
     const PairT* pairs;
@@ -171,9 +171,6 @@ struct Enc {
     const PairT* ovf;
     uint64_t gbase;
     uint32_t ring_base;
-    // ---- RangeEncoder (RangeEncoder.java:9-14)
-    uint64_t low;
-    uint32_t range, cache_size, cache;
     // ---- Encoder fields (Encoder.java:132-181)
     uint32_t mfpos;           // match-finder position, 0-based (BinTree._pos - 1)
     int32_t additional_offset, opt_end, opt_cur;
@@ -379,31 +376,28 @@ struct Enc {
         return r + match_len(o + (int32_t)r - 1, dist, limit - (int32_t)r);
     }
 
-    // ------------------------------------------------------------ range encoder (RangeEncoder.java:38-87)
-    // Output bytes are staged in LDS and written kObuf at a time by all lanes:
-    // a global store per byte would make the next dependent load wait for it
-    // (vmcnt counts stores and loads alike on CDNA).
-    FI void flush_out(uint32_t start, uint32_t count) {
-        LANE_FENCE();
-        LANE_FOR(uint32_t, i, 0u, count)
-            if (start + i < cap) __builtin_nontemporal_store(obuf[i], out + start + i);
-        LANE_FENCE();
+    // ------------------------------------------------------------ coder records
+    // The range coder (RangeEncoder.java:38-87) does not feed back into the
+    // parse: its arithmetic needs only each decision's probability before the
+    // update and the bit. The parser therefore emits one 16-bit record per
+    // binary decision (prob | bit << 11; prob 0 = a direct bit) and rc.hip runs
+    // the coder arithmetic, one lane per stream, on the vector unit. Records
+    // are staged in LDS and written 64 at a time by 32 lanes (one 128-byte
+    // store): a global store per symbol would make the next dependent load
+    // wait for it (vmcnt counts stores and loads alike on CDNA).
+    FI void rec_store_block(uint64_t blk) {   // records [blk * 64, blk * 64 + 64): a full half of the ring
+        if ((blk + 1) * 64 > rcap) { overflow = 1; return; }
+        const uint32_t* src = (const uint32_t*)(rbuf + (blk & 1) * 64);
+        uint32_t* dst = (uint32_t*)(recs + blk * 64);
+        LANE_FOR(uint32_t, w, 0u, 32u) __builtin_nontemporal_store(src[w], dst + w);
     }
-    FI void put_byte(uint32_t b) {
-        if (outpos >= cap) overflow = 1;
-        if (lane == 0) obuf[outpos & (kObuf - 1)] = (uint8_t)b;
-        outpos++;
-        if ((outpos & (kObuf - 1)) == 0) flush_out(outpos - kObuf, kObuf);
-    }
-    FI void shift_low() {
-        uint32_t hi = (uint32_t)(low >> 32);
-        if (hi != 0 || low < 0xFF000000ull) {
-            uint32_t temp = cache;
-            do { put_byte((temp + hi) & 0xFF); temp = 0xFF; } while (--cache_size != 0);
-            cache = ((uint32_t)low) >> 24;
-        }
-        cache_size++;
-        low = (low & 0xFFFFFFull) << 8;
+    FI void rec_store_tail() {   // the partial block at the end of the stream
+        const uint64_t blk = rpos >> 6;
+        const uint32_t cnt = (uint32_t)rpos & 63u;
+        if (cnt == 0) return;
+        if (blk * 64 + cnt > rcap) { overflow = 1; return; }
+        LANE_FOR(uint32_t, k, 0u, cnt) __builtin_nontemporal_store(rbuf[(blk & 1) * 64 + k], recs + blk * 64 + k);
+        LANE_FENCE();
     }
     // ------------------------------------------------------------ symbol coder
     // One coded symbol (literal, rep, match or the end marker) is the sequence
@@ -504,30 +498,17 @@ struct Enc {
     }
     FI void q_run(const Q& q) {
         uint32_t pr[kQS];
-        uint64_t bm = 0, dm = 0;
 #pragma unroll
         for (int t = 0; t < kQS; t++) {
             pr[t] = 0;
             if (q.kind[t] == QK_LIT) pr[t] = lit[q.idx[t]];
             else if (q.kind[t] == QK_PROB) pr[t] = probs[q.idx[t]];
-            bm |= (uint64_t)__ballot(q.bit[t] != 0) << (t * kWave);
-            dm |= (uint64_t)__ballot(q.kind[t] == QK_DIRECT) << (t * kWave);
         }
-#pragma unroll 1
-        for (uint32_t j = 0; j < q.n; j++) {
-            const uint32_t b = (uint32_t)(bm >> j) & 1u;
-            if ((dm >> j) & 1u) {
-                range >>= 1;
-                if (b) low += range;
-            } else {
-                const uint32_t bound = (range >> 11) * lane_value(pr, (int)j);
-                if (b) { low += bound; range -= bound; }
-                else range = bound;
-            }
-            if ((range & kTopMask) == 0) { range <<= 8; shift_low(); }
-        }
+        const uint32_t base = (uint32_t)rpos;
 #pragma unroll
         for (int t = 0; t < kQS; t++) {
+            const uint32_t j = (uint32_t)(t * kWave) + lane;
+            if (j < q.n) rbuf[(base + j) & (kRbuf - 1)] = (uint16_t)((q.kind[t] == QK_DIRECT ? 0u : pr[t]) | (q.bit[t] << 11));
             const uint32_t p = pr[t];
             const uint16_t np = (uint16_t)(q.bit[t] ? p - (p >> kNumMoveBits) : p + ((kBitModelTotal - p) >> kNumMoveBits));
 #ifdef LZG_ABL_LITSTORE
@@ -541,6 +522,9 @@ struct Enc {
             }
         }
         LANE_FENCE();
+        const uint64_t p0 = rpos;
+        rpos += q.n;   // q.n <= 48 < 64: at most one block completes per symbol
+        if ((p0 >> 6) != (rpos >> 6)) rec_store_block(p0 >> 6);
     }
 
     // ------------------------------------------------------------ price tables
@@ -1200,11 +1184,9 @@ struct Enc {
             if (c == 0) update_len_table(len_coder, ps);
         }
     }
-    FI void flush(uint32_t now_pos) {
+    FI void flush(uint32_t now_pos) {   // the coder's own flush (5 x ShiftLow) runs in rc.hip
         if (eos) encode_symbol(0, kMatchMinLen, now_pos, prev_byte, 0, true);
-#pragma unroll 1
-        for (int i = 0; i < 5; i++) shift_low();
-        flush_out(outpos & ~(uint32_t)(kObuf - 1), outpos & (kObuf - 1));
+        rec_store_tail();
     }
 
     FI void run() {   // Encoder.Code: SetStreams + CodeOneBlock/encodeOne (Encoder.java:843-936, 1046-1077)
@@ -1221,7 +1203,7 @@ struct Enc {
         state = 0; prev_byte = 0;
         rd0 = rd1 = rd2 = rd3 = 0;
         rp0 = rp1 = rp2 = rp3 = 0;
-        low = 0; range = 0xFFFFFFFFu; cache_size = 1; cache = 0; outpos = 0; overflow = 0; bad = 0;
+        rpos = 0; overflow = 0; bad = 0;
         wd = 0; wd_max = n < 0x50000000u ? 3 * n + 4096 : 0xFFFFFFFFu;   // iterations <= 2n + calls
         longest_found = 0; opt_end = 0; opt_cur = 0; additional_offset = 0;
         longest_len = 0; num_pairs = 0; mfpos = 0;
@@ -1293,13 +1275,13 @@ struct Enc {
 // LDS layout of one stream's workgroup; shared by the kernel (carving) and
 // the host (dynamic LDS size). Regions are 16-byte aligned.
 enum { L_PP, L_PROBS, L_DMP, L_LENP, L_LENC, L_PSP, L_DP, L_AP, L_TP, L_MDLEN, L_MDDIST, L_RINFO, L_RPAIRS, L_OPRICE,
-       L_OPP, L_OBP, L_OBP2, L_OFS, L_OBACKS, L_OBYTES, L_WIN, L_OBUF, L_LIT, L_COUNT };
+       L_OPP, L_OBP, L_OBP2, L_OFS, L_OBACKS, L_OBYTES, L_WIN, L_RBUF, L_LIT, L_COUNT };
 __host__ __device__ inline uint32_t enc_lds_layout(const EncArgs& a, uint32_t* off) {
     const uint32_t md_cap = a.fb + 2;   // pairs per position <= fb (+1 clamp slot)
     const uint32_t sz[L_COUNT] = {
         512 * 2, prob_count(a.pb) * 2, dm_count(a.pb) * 4, 2 * (1u << a.pb) * a.len_table_size * 2, 2 * 16 * 4, 256 * 2, 512 * 2, 16 * 4,
         0u /* tp aliases the gather window */, md_cap * 2, md_cap * 4, kRing * 4, kRing * kInlinePairs * a.pair_bytes, kOptLds * 4, kOptLds * 4,
-        kOptLds * 4, kOptLds * 4, kOptLds, 4 * kOptLds * 4, kOptLds * 4, kSides * kGW, kObuf,
+        kOptLds * 4, kOptLds * 4, kOptLds, 4 * kOptLds * 4, kOptLds * 4, kSides * kGW, kRbuf * 2,
         a.lit_in_lds ? (0x300u << (a.lc + a.lp)) * 2 : 0u};
     uint32_t o = 0;
     for (int i = 0; i < L_COUNT; i++) { if (off) off[i] = o; o += (sz[i] + 15) & ~15u; }
@@ -1347,7 +1329,7 @@ __global__ void __launch_bounds__(kWave, 4) enc_kernel(EncArgs a) {
     e.o_backs = (uint32_t*)(smem + off[L_OBACKS]);
     e.o_bytes = (uint32_t*)(smem + off[L_OBYTES]);
     e.win = smem + off[L_WIN];
-    e.obuf = smem + off[L_OBUF];
+    e.rbuf = (uint16_t*)(smem + off[L_RBUF]);
     uint8_t* scratch = a.scratch + (size_t)blockIdx.x * a.scratch_stride;
     e.spill = __builtin_amdgcn_make_buffer_rsrc(scratch, 0, kNumOpts * 4 * 10, 0x00020000);
     uint16_t* lit_g = (uint16_t*)(a.lit_scratch + (size_t)blockIdx.x * a.lit_stride);
@@ -1373,10 +1355,9 @@ __global__ void __launch_bounds__(kWave, 4) enc_kernel(EncArgs a) {
     e.n = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(uni64(a.offs[s + 1]) - e.gbase));
     e.in = a.in + e.gbase;
     e.inb = __builtin_amdgcn_make_buffer_rsrc((void*)e.in, 0, e.n, 0x00020000);
-    const uint64_t oo = uni64(a.out_offs[s]);
-    e.out = a.out + oo;
-    const uint64_t cap64 = uni64(a.out_offs[s + 1]) - oo;
-    e.cap = cap64 > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)cap64;   // any stream's output is < 4 GiB
+    const uint64_t ro = uni64(a.rec_offs[s]);
+    e.recs = a.recs + ro;
+    e.rcap = uni64(a.rec_offs[s + 1]) - ro;
 #ifdef LZG_DEBUG
     if (e.dbg && e.lane == 0) __hip_atomic_store(e.dbg + 8, (uint32_t)s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 #endif
@@ -1395,9 +1376,11 @@ __global__ void __launch_bounds__(kWave, 4) enc_kernel(EncArgs a) {
     if (e.lane == 0 && a.prof)
         for (int k = 0; k < kProfSlots; k++) a.prof[(size_t)s * kProfSlots + k] = e.prof[k];
 #endif
+    if (e.overflow && !e.bad) e.bad = 7;   // record region smaller than rc_record_bound(): a bug, not the data
     if (e.lane == 0) {
-        a.out_lens[s] = e.bad ? (((uint64_t)e.bad << 32) | e.mfpos) : (uint64_t)e.outpos;
-        a.status[s] = e.bad ? LZMA_E_INTERNAL : (e.overflow ? LZMA_E_OVERFLOW : LZMA_OK);
+        a.rec_lens[s] = e.rpos;
+        if (e.bad) a.out_lens[s] = ((uint64_t)e.bad << 32) | e.mfpos;
+        a.status[s] = e.bad ? LZMA_E_INTERNAL : LZMA_OK;
     }
 }
 

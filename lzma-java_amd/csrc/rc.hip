@@ -1,0 +1,209 @@
+// rc.hip -- the range coder of src/main/java/SevenZip/Compression/RangeCoder/
+// Encoder.java (RangeEncoder.java:18-87) run over the parser's coder records.
+//
+// enc.hip emits one 16-bit record per binary decision of the symbol coder:
+// the probability before its update (11 bits) and the bit (bit 11); a record
+// with probability 0 is a direct bit (EncodeDirectBits, :56-67). The coder's
+// arithmetic never feeds back into the parse, so it runs here, after the
+// parse, one LANE per stream: the serial chain of every stream runs on the
+// vector unit (64 streams per wave instruction) instead of the single scalar
+// unit of a CU that the 16 parser waves already share.
+//
+// A stream's chain is serial, so the kernel time is one stream's chain
+// latency. The step is therefore straight-line code over a block of 64
+// records (no branches: the compiler interleaves the next record's range
+// update with this record's low/output bookkeeping):
+//   * `low` is 32 bits plus a carry bit: after ShiftLow low < 2^32, and the
+//     bounds added before the next ShiftLow sum to less than the range;
+//   * output bytes go to a per-lane LDS ring with unconditional writes: the
+//     cache byte at outpos and one pending 0xFF/0x00 byte after it (positions
+//     >= outpos are not final yet, so a write there that turns out not to be
+//     an emission is overwritten later);
+//   * after each block the ring goes to HBM as 18 aligned dwords into the
+//     stream's own record region, which serves as the output staging area: a
+//     record is 2 bytes and makes at most one byte, so output position k is
+//     always far behind the records still to be read; rc_copy_kernel then
+//     copies each stream's bytes to the caller's output layout;
+//   * a pending run of two or more 0xFF bytes (cacheSize > 2 at an emission,
+//     about once per 2^16 shifts) only sets a flag: lanes that raised it replay
+//     the block from the saved state with the exact reference step, writing
+//     straight to HBM.
+#include "lzma_common.h"
+#include "runtime.h"
+
+namespace lzg {
+
+constexpr int kRcRing = 72;             // bytes per lane: a block starts <= 3 bytes past its base and emits <= 66
+constexpr int kRcStride = kRcRing + 4;  // 19 dwords: lane rings start in distinct LDS banks
+constexpr int kRcLanes = 64;
+
+struct RcState {
+    uint32_t lo, carry, range, cache, cache_size;
+    uint32_t outpos;   // streams < 2 GiB: outputs < 4 GiB
+};
+
+struct RcLane : RcState {
+    uint8_t* stage;    // output staging: the stream's record region
+    uint8_t* ring;     // this lane's ring: byte k is output position base + k
+
+    uint32_t tailw;    // the staged dword holding position outpos - 1 (kept by put)
+
+    // ---- exact reference step (replay and stream tail): bytes straight to the staging area
+    __device__ __forceinline__ void put(uint32_t b) {
+        const uint32_t sh = (outpos & 3u) * 8;
+        tailw = (tailw & ~(0xFFu << sh)) | ((b & 0xFFu) << sh);
+        stage[outpos++] = (uint8_t)b;
+    }
+    __device__ __forceinline__ void shift_low() {   // RangeEncoder.ShiftLow (:73-87)
+        if (carry != 0 || lo < 0xFF000000u) {
+            uint32_t temp = cache;
+#pragma unroll 1
+            do { put((temp + carry) & 0xFFu); temp = 0xFF; } while (--cache_size != 0);
+            cache = lo >> 24;
+        }
+        cache_size++;
+        lo = (lo & 0xFFFFFFu) << 8;
+        carry = 0;
+    }
+    // Encode (:38-54) for prob != 0, one EncodeDirectBits step (:56-67) for prob == 0
+    __device__ __forceinline__ void step_exact(uint32_t rec) {
+        const uint32_t p = rec & 0x7FFu, bit = (rec >> 11) & 1u;
+        const uint32_t bound = p ? (range >> 11) * p : range >> 1;
+        if (bit) {
+            const uint32_t nl = lo + bound;
+            carry |= nl < lo;
+            lo = nl;
+        }
+        range = (bit && p) ? range - bound : bound;
+        if (range < (1u << 24)) { range <<= 8; shift_low(); }
+    }
+
+    // ---- fast step: selects and unconditional ring writes only
+    __device__ __forceinline__ void step_fast(uint32_t rec, uint32_t base, bool& flag) {
+        const uint32_t p = rec & 0x7FFu;
+        const bool bit = (rec & 0x800u) != 0, direct = p == 0;
+        const uint32_t bp = (range >> 11) * p, bd = range >> 1;
+        const uint32_t bound = direct ? bd : bp;
+        const uint32_t r1 = (bit && !direct) ? range - bp : bound;
+        const bool norm = r1 < (1u << 24);
+        range = norm ? r1 << 8 : r1;
+        const uint32_t add = bit ? bound : 0u;
+        const uint32_t l = lo + add;
+        const uint32_t c = carry + (l < add ? 1u : 0u);   // at most one carry between two ShiftLows
+        // ShiftLow when norm: the cache group [outpos, outpos + cache_size) leaves when the
+        // carry is known (carry set or the top byte < 0xFF)
+        const uint32_t top = l >> 24;
+        const bool emit = norm && ((c << 8) | top) != 0xFFu;
+        flag |= emit && cache_size > 2;
+#ifdef LZG_RC_FORCE_REPLAY
+        flag = true;   // test builds: every block takes the exact replay path
+#endif
+        ring[outpos - base] = (uint8_t)(cache + c);
+        ring[outpos - base + 1] = (uint8_t)(0xFFu + c);
+        outpos += emit ? cache_size : 0u;
+        cache = emit ? top : cache;
+        cache_size = emit ? 1u : cache_size + (norm ? 1u : 0u);
+        lo = norm ? l << 8 : l;
+        carry = norm ? 0u : c;
+    }
+};
+
+__device__ __forceinline__ uint32_t rec_at(const uint32_t (&w)[32], int k) {
+    return (w[k >> 1] >> ((k & 1) * 16)) & 0xFFFFu;
+}
+
+__global__ void __launch_bounds__(kRcLanes) rc_kernel(RcArgs a) {
+    __shared__ __attribute__((aligned(16))) uint32_t rings[kRcLanes * kRcStride / 4];
+    const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (i >= a.nstreams) return;
+    const uint32_t s = a.order[i];
+    if (a.status[s] != LZMA_OK) return;
+    const uint64_t n = a.rec_lens[s];
+    uint16_t* region = a.recs + a.rec_offs[s];   // 64-record (128-byte) aligned
+    const uint32_t* r32 = (const uint32_t*)region;
+    uint32_t* ring32 = rings + threadIdx.x * (kRcStride / 4);
+    uint32_t* stage32 = (uint32_t*)region;
+    RcLane c;
+    c.stage = (uint8_t*)region;
+    c.ring = (uint8_t*)ring32;
+    c.outpos = 0;
+    c.tailw = 0;
+    c.lo = 0; c.carry = 0; c.range = 0xFFFFFFFFu; c.cache = 0; c.cache_size = 1;   // Init (:18-24)
+    // blocks of 64 records (32 dwords per lane); the next block's loads are issued
+    // before this block is coded, so their HBM latency overlaps the coding
+    const uint64_t nblk = (n + 63) >> 6, full = n >> 6;
+    uint32_t cur[32], nxt[32];
+    if (nblk) {
+#pragma unroll
+        for (int j = 0; j < 32; j++) cur[j] = __builtin_nontemporal_load(r32 + j);
+    }
+    uint32_t base = 0;   // the ring's first byte is output position base (a multiple of 4)
+    for (uint64_t b = 0; b < nblk; b++) {
+        if (b + 1 < nblk) {
+#pragma unroll
+            for (int j = 0; j < 32; j++) nxt[j] = __builtin_nontemporal_load(r32 + (b + 1) * 32 + j);
+        }
+        if (b < full) {
+            // carry the final bytes [nb, outpos) of the last partial dword to the ring start
+            const uint32_t nb = c.outpos & ~3u;
+            ring32[0] = ring32[(nb - base) >> 2];
+            c.tailw = ring32[0];
+            base = nb;
+            const RcState saved = c;
+            bool flag = false;
+#pragma unroll
+            for (int k = 0; k < 64; k++) c.step_fast(rec_at(cur, k), base, flag);
+            if (__builtin_amdgcn_ballot_w64(flag) && flag) {   // rare: replay the block exactly
+                (RcState&)c = saved;
+#pragma unroll 1
+                for (int k = 0; k < 64; k++) c.step_exact(rec_at(cur, k));
+                // the ring restarts at the replay's last partial dword (its final bytes: tailw)
+                base = c.outpos & ~3u;
+                ring32[0] = c.tailw;
+            } else {
+                // all 18 ring dwords: positions past outpos are not final and are rewritten
+                // later; they stay below the records not yet read
+#pragma unroll
+                for (int j = 0; j < kRcRing / 4; j++) stage32[(base >> 2) + j] = ring32[j];
+            }
+        } else {
+            const uint32_t m = (uint32_t)(n & 63);
+#pragma unroll 1
+            for (uint32_t k = 0; k < m; k++) c.step_exact(rec_at(cur, (int)k));
+        }
+#pragma unroll
+        for (int j = 0; j < 32; j++) cur[j] = nxt[j];
+    }
+#pragma unroll 1
+    for (int k = 0; k < 5; k++) c.shift_low();   // FlushData (:31-36)
+    const uint64_t cap = a.out_offs[s + 1] - a.out_offs[s];
+    a.out_lens[s] = c.outpos;
+    if (c.outpos > cap) a.status[s] = LZMA_E_OVERFLOW;
+}
+
+// staged bytes of each stream to the caller's output layout: one block per stream
+__global__ void __launch_bounds__(256) rc_copy_kernel(RcArgs a) {
+    const uint32_t s = blockIdx.x;
+    if (a.status[s] != LZMA_OK) return;
+    const uint8_t* src = (const uint8_t*)(a.recs + a.rec_offs[s]);
+    uint8_t* dst = a.out + a.out_offs[s];
+    const uint64_t len = a.out_lens[s];
+    for (uint64_t k = threadIdx.x; k < len; k += blockDim.x) dst[k] = src[k];
+}
+
+int launch_rc(Ctx* ctx, const RcArgs& a, hipStream_t st) {
+    if (a.nstreams <= 0) return LZMA_OK;
+    {
+        TimedLaunch tl(ctx, "enc_rc", st);
+        hipLaunchKernelGGL(rc_kernel, dim3((a.nstreams + kRcLanes - 1) / kRcLanes), dim3(kRcLanes), 0, st, a);
+    }
+    {
+        TimedLaunch tl(ctx, "enc_rc_copy", st);
+        hipLaunchKernelGGL(rc_copy_kernel, dim3(a.nstreams), dim3(256), 0, st, a);
+    }
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return ctx->fail(LZMA_E_DEVICE, "rc launch: %s", hipGetErrorString(e));
+    return LZMA_OK;
+}
+
+}  // namespace lzg

@@ -224,9 +224,10 @@ struct EncArgs {
     const void* pairs;
     const uint32_t* ovf_off;
     const void* ovf;
-    uint8_t* out;
-    const uint64_t* out_offs;     // capacity layout (nstreams+1)
-    uint64_t* out_lens;
+    uint16_t* recs;               // coder records (rc.hip), per stream at rec_offs[s]
+    const uint64_t* rec_offs;     // record capacity layout (nstreams+1), multiples of 64 records
+    uint64_t* rec_lens;           // records emitted per stream
+    uint64_t* out_lens;           // diagnostic (reason << 32 | position) of streams that tripped a check
     int32_t* status;
     uint8_t* scratch;             // per-block global scratch (_optimum spill)
     uint64_t scratch_stride;
@@ -244,6 +245,23 @@ enum { PF_TOTAL, PF_GETOPT, PF_MATCHES, PF_REPLEN, PF_TWOLEN, PF_LIT, PF_RELAX, 
        PF_ENCODE, PF_TABLES, PF_NOPT, PF_NPOS, PF_T0, PF_T1, PF_HWID, kProfSlots };
 
 int launch_encoder(Ctx* ctx, const EncArgs& a, bool wide_pairs, int grid, hipStream_t st);
+
+// rc.hip: the range coder over the parser's records, one lane per stream
+struct RcArgs {
+    uint16_t* recs;               // read, then reused as each stream's output staging
+    const uint64_t* rec_offs;
+    const uint64_t* rec_lens;
+    const uint32_t* order;        // longest first: the lanes of a wave get similar record counts
+    int nstreams;
+    int32_t* status;              // in: the parser's verdict; out: LZMA_E_OVERFLOW when the output does not fit
+    uint8_t* out;
+    const uint64_t* out_offs;     // output capacity layout (nstreams+1)
+    uint64_t* out_lens;
+};
+int launch_rc(Ctx* ctx, const RcArgs& a, hipStream_t st);
+// records one stream of n bytes can need: <= 21 per byte (a length-2 match: isMatch, isRep,
+// 4 length bits, 6 slot bits, 30 footer bits), the end marker (42) and the first literal
+__host__ __device__ inline uint64_t rc_record_bound(uint64_t n) { return (24 * n + 64 + 63) & ~(uint64_t)63; }
 uint32_t enc_lit_in_lds(const Derived& d);
 size_t enc_scratch_per_block(const Derived& d);
 size_t enc_lit_bytes(const Derived& d);

@@ -126,8 +126,32 @@ static int encode_pass(Ctx* ctx, const Derived& d, const uint8_t* d_in, const ui
         return slots * stride;
     };
     uint64_t ovf_cap = pool_cap(slots_per_k);
+    // coder records (rc.hip) per stream: capacity layout in records, 64-record aligned
+    std::vector<uint64_t> rofs(ns + 1, 0);
+    for (int i = 0; i < ns; i++) rofs[i + 1] = rofs[i] + rc_record_bound(offs[i + 1] - offs[i]);
     for (int attempt = 0; attempt < 6; attempt++) {
         const uint64_t T = total;
+        // buffers only the match finder uses; the coder records reuse their memory after the walk
+        auto phase1 = [&](Carver& c, MfBuffers& w) {
+            w.k4 = c.take<uint64_t>(T); w.k3 = c.take<uint64_t>(T); w.k2 = c.take<uint64_t>(T); w.ks = c.take<uint64_t>(T);
+            w.vals = c.take<uint32_t>(T); w.vs = c.take<uint32_t>(T);
+            w.prev2 = c.take<uint32_t>(T); w.prev3 = c.take<uint32_t>(T);
+            w.flag = c.take<uint8_t>(T);
+            w.chain_start = c.take<uint32_t>(T); w.chain_len = c.take<uint32_t>(T); w.chain_len_sorted = c.take<uint32_t>(T);
+            w.chain_idx = c.take<uint32_t>(T); w.chain_order = c.take<uint32_t>(T);
+            w.counts = c.take<uint64_t>(2);
+            w.son = c.take<uint64_t>(4 * T);   // mf.hip WNode: 32 bytes per position
+        };
+        size_t p1_bytes;
+        {
+            MfBuffers pw{};
+            Carver probe(nullptr);
+            phase1(probe, pw);
+            p1_bytes = probe.off;
+        }
+        const size_t union_bytes = std::max<size_t>(p1_bytes, rofs[ns] * 2);
+        uint16_t* d_recs = nullptr;
+        uint64_t *d_rofs = nullptr, *d_rlens = nullptr;
         auto need = [&](Carver& c, MfBuffers& w, uint8_t** inpad, uint64_t** d_offs, uint64_t** d_oofs,
                         uint32_t** d_order, uint64_t** d_lens, int32_t** d_status, unsigned** d_next, uint8_t** d_scr) {
             *inpad = c.take<uint8_t>(T + 512);
@@ -137,14 +161,13 @@ static int encode_pass(Ctx* ctx, const Derived& d, const uint8_t* d_in, const ui
             *d_lens = c.take<uint64_t>(ns);
             *d_status = c.take<int32_t>(ns);
             *d_next = c.take<unsigned>(4);
-            w.k4 = c.take<uint64_t>(T); w.k3 = c.take<uint64_t>(T); w.k2 = c.take<uint64_t>(T); w.ks = c.take<uint64_t>(T);
-            w.vals = c.take<uint32_t>(T); w.vs = c.take<uint32_t>(T); w.minfo = c.take<uint32_t>(T);
-            w.prev2 = c.take<uint32_t>(T); w.prev3 = c.take<uint32_t>(T);
-            w.flag = c.take<uint8_t>(T);
-            w.chain_start = c.take<uint32_t>(T); w.chain_len = c.take<uint32_t>(T); w.chain_len_sorted = c.take<uint32_t>(T);
-            w.chain_idx = c.take<uint32_t>(T); w.chain_order = c.take<uint32_t>(T);
-            w.counts = c.take<uint64_t>(2);
-            w.son = c.take<uint64_t>(4 * T);   // mf.hip WNode: 32 bytes per position
+            d_rofs = c.take<uint64_t>(ns + 1);
+            d_rlens = c.take<uint64_t>(ns);
+            uint8_t* u = c.take<uint8_t>(union_bytes);
+            d_recs = (uint16_t*)u;
+            Carver c1(u);
+            phase1(c1, w);
+            w.minfo = c.take<uint32_t>(T);
             w.pairs = c.take<uint8_t>(T * kInlinePairs * psz);
             w.ovf_off = c.take<uint32_t>(T);
             w.ovf = c.take<uint8_t>(ovf_cap * psz);
@@ -173,6 +196,7 @@ static int encode_pass(Ctx* ctx, const Derived& d, const uint8_t* d_in, const ui
             HIPCHK(hipMemcpyAsync(d_offs, offs.data(), (ns + 1) * 8, hipMemcpyHostToDevice, st));
             HIPCHK(hipMemcpyAsync(d_oofs, oofs.data(), (ns + 1) * 8, hipMemcpyHostToDevice, st));
             HIPCHK(hipMemcpyAsync(d_order, order.data(), ns * 4, hipMemcpyHostToDevice, st));
+            HIPCHK(hipMemcpyAsync(d_rofs, rofs.data(), (ns + 1) * 8, hipMemcpyHostToDevice, st));
             HIPCHK(hipMemsetAsync(d_next, 0, 16, st));
         }
         int rc = run_match_finder(ctx, d, inpad, d_offs, ns, total, wide, w, st);
@@ -206,7 +230,7 @@ static int encode_pass(Ctx* ctx, const Derived& d, const uint8_t* d_in, const ui
         EncArgs a{};
         a.in = inpad; a.offs = d_offs; a.order = d_order; a.nstreams = ns; a.next = d_next;
         a.minfo = w.minfo; a.pairs = w.pairs; a.ovf_off = w.ovf_off; a.ovf = w.ovf;
-        a.out = d_out; a.out_offs = d_oofs; a.out_lens = d_lens; a.status = d_status;
+        a.recs = d_recs; a.rec_offs = d_rofs; a.rec_lens = d_rlens; a.out_lens = d_lens; a.status = d_status;
         a.scratch = d_scr; a.scratch_stride = scr;
         a.lit_stride = (enc_lit_bytes(d) + 255) & ~(size_t)255;
         if (!ctx->ensure_litbuf((size_t)grid * a.lit_stride + 256)) return ctx->fail(LZMA_E_NOMEM, "literal-coder tables");
@@ -227,6 +251,11 @@ static int encode_pass(Ctx* ctx, const Derived& d, const uint8_t* d_in, const ui
         if ((rc = launch_encoder(ctx, a, wide, grid, st))) return rc;
         LZG_TRACE(ctx, st, "enc_parse done");
         watch.stop();
+        RcArgs ra{};
+        ra.recs = d_recs; ra.rec_offs = d_rofs; ra.rec_lens = d_rlens; ra.order = d_order; ra.nstreams = ns;
+        ra.status = d_status; ra.out = d_out; ra.out_offs = d_oofs; ra.out_lens = d_lens;
+        if ((rc = launch_rc(ctx, ra, st))) return rc;
+        LZG_TRACE(ctx, st, "enc_rc done");
 #ifdef LZG_PROF
         report_profile(d_prof, ns, total, st);
         hipFree(d_prof);

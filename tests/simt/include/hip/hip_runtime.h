@@ -212,6 +212,10 @@ inline unsigned long long __ballot(int pred) {
     ::hipemu::barrier();
     return m;
 }
+// rc.hip uses the raw ballot only as a wave-uniform "any lane" skip around code that is a
+// no-op for lanes whose predicate is false, so the lane's own predicate is exact here (and
+// needs no barrier: rc.hip lanes leave their loops at different times)
+inline unsigned long long __builtin_amdgcn_ballot_w64(bool p) { return p ? 1ull : 0ull; }
 #define __builtin_amdgcn_fence(order, scope) __atomic_signal_fence(__ATOMIC_SEQ_CST)
 // wave width 1: the first active lane is the only lane
 inline int __builtin_amdgcn_readfirstlane(int v) { return v; }
