@@ -444,18 +444,19 @@ int run_match_finder(Ctx* ctx, const Derived& d, const uint8_t* in, const uint64
         const unsigned prev_grid = (unsigned)(((total + B - 1) / B + 7) & ~7ull);   // total < 2^32: fits
         {
             TimedLaunch tl(ctx, "mf_sort", st);
-            if ((rc = segmented_sort(ctx, (uint32_t*)w.k2, (uint32_t*)w.ks, w.vals, w.vs, total, d_offs, nstreams, 10, st))) return rc;
+            if ((rc = seg_radix_sort(ctx, false, w.k2, w.vals, w.ks, w.vs, w.son, w.son + total, w.hist, total, d_offs, nstreams, 10, st))) return rc;
         }
         hipLaunchKernelGGL(mf_prev_kernel, dim3(prev_grid), dim3(B), 0, st, (const uint32_t*)w.ks, w.vs, total, w.prev2);
         {
             TimedLaunch tl(ctx, "mf_sort", st);
-            if ((rc = segmented_sort(ctx, (uint32_t*)w.k3, (uint32_t*)w.ks, w.vals, w.vs, total, d_offs, nstreams, 16, st))) return rc;
+            if ((rc = seg_radix_sort(ctx, false, w.k3, w.vals, w.ks, w.vs, w.son, w.son + total, w.hist, total, d_offs, nstreams, 16, st))) return rc;
         }
         hipLaunchKernelGGL(mf_prev_kernel, dim3(prev_grid), dim3(B), 0, st, (const uint32_t*)w.ks, w.vs, total, w.prev3);
     }
     {
         TimedLaunch tl(ctx, "mf_sort", st);
-        if ((rc = segmented_sort(ctx, w.k4, w.ks, w.vals, w.vs, total, d_offs, nstreams, (int)(bt4 ? d.hash_bits : 16), st))) return rc;
+        if ((rc = seg_radix_sort(ctx, true, w.k4, w.vals, w.ks, w.vs, w.son, w.son + total, w.hist, total, d_offs, nstreams,
+                                 (int)(bt4 ? d.hash_bits : 16), st))) return rc;
     }
     hipMemsetAsync(w.counts, 0, 2 * sizeof(uint64_t), st);   // [0]=nvalid [1]=nchains
     hipLaunchKernelGGL(mf_heads_kernel, dim3(grid_for(total, B)), dim3(B), 0, st, w.ks, total, w.flag, w.counts);

@@ -35,7 +35,9 @@ struct MfBuffers {
     uint8_t* flag;
     uint32_t *chain_start, *chain_len, *chain_len_sorted, *chain_idx, *chain_order;
     uint64_t* counts;
-    uint64_t* son;                // walk tree nodes (mf.hip WNode, 32 B per position: links + 16-byte prefix)
+    uint64_t* son;                // walk tree nodes (mf.hip WNode, 32 B per position: links + 16-byte prefix);
+                                  // before the walk, the sorts' ping-pong buffers
+    uint32_t* hist;               // sort.hip digit histograms, [nstreams][4][256]
     void* pairs;
     uint32_t* ovf_off;
     void* ovf;
@@ -213,6 +215,10 @@ __host__ __device__ inline uint32_t ovf_stride(uint32_t fb) { return fb > (uint3
 
 int run_match_finder(Ctx* ctx, const Derived& d, const uint8_t* in, const uint64_t* d_offs, int nstreams,
                      uint64_t total, bool wide_pairs, MfBuffers& w, hipStream_t st);
+// sort.hip: stable per-stream radix sort by the low end_bit key bits
+int seg_radix_sort(Ctx* ctx, bool key64, const void* kin, const uint32_t* vin, void* kout, uint32_t* vout,
+                   uint64_t* tmp_a, uint64_t* tmp_b, uint32_t* hist, uint64_t n, const uint64_t* d_offs, int nstreams,
+                   int end_bit, hipStream_t st);
 
 struct EncArgs {
     const uint8_t* in;            // padded batch copy

@@ -141,6 +141,7 @@ static int encode_pass(Ctx* ctx, const Derived& d, const uint8_t* d_in, const ui
             w.chain_idx = c.take<uint32_t>(T); w.chain_order = c.take<uint32_t>(T);
             w.counts = c.take<uint64_t>(2);
             w.son = c.take<uint64_t>(4 * T);   // mf.hip WNode: 32 bytes per position
+            w.hist = c.take<uint32_t>((size_t)ns * 1024);
         };
         size_t p1_bytes;
         {

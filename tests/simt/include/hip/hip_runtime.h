@@ -216,6 +216,18 @@ inline unsigned long long __ballot(int pred) {
 // no-op for lanes whose predicate is false, so the lane's own predicate is exact here (and
 // needs no barrier: rc.hip lanes leave their loops at different times)
 inline unsigned long long __builtin_amdgcn_ballot_w64(bool p) { return p ? 1ull : 0ull; }
+// wave barrier: a block barrier here (the emulated lanes of a wave are not in lockstep)
+#define __builtin_amdgcn_wave_barrier() ::hipemu::barrier()
+// mbcnt: set bits of the mask below this lane's index within its 64-lane group
+inline uint32_t __builtin_amdgcn_mbcnt_lo(uint32_t m, uint32_t acc) {
+    const unsigned l = threadIdx.x & 63u;
+    return acc + (uint32_t)__builtin_popcount(l >= 32 ? m : (m & ((1u << l) - 1u)));
+}
+inline uint32_t __builtin_amdgcn_mbcnt_hi(uint32_t m, uint32_t acc) {
+    const unsigned l = threadIdx.x & 63u;
+    return acc + (uint32_t)(l < 32 ? 0 : __builtin_popcount(m & (l == 32 ? 0u : ((1u << (l - 32)) - 1u))));
+}
+inline unsigned atomicAdd(unsigned* p, unsigned v);
 #define __builtin_amdgcn_fence(order, scope) __atomic_signal_fence(__ATOMIC_SEQ_CST)
 // wave width 1: the first active lane is the only lane
 inline int __builtin_amdgcn_readfirstlane(int v) { return v; }
