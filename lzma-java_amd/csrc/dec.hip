@@ -116,12 +116,25 @@ struct Dec {
     // RangeDecoder.DecodeBit (RangeDecoder.java:43-64) on a probability already
     // in a register; *np = the adapted probability
     // (branch-free selects: the scalar unit is the decoder's bottleneck)
+    // The adapted probability only feeds a store, so it is computed on the vector
+    // unit (vgpr(): a v_mov the compiler must treat as per-lane), off the scalar chain.
+    static DFI uint32_t vgpr(uint32_t x) {
+#if LZG_WAVE == 64
+        uint32_t y;
+        asm volatile("v_mov_b32 %0, %1" : "=v"(y) : "v"(x));
+        return y;
+#else
+        return x;
+#endif
+    }
     DFI uint32_t dbit(uint32_t prob, uint32_t* np) {
         const uint32_t bound = (range >> 11) * prob;
         const bool one = code >= bound;
         range = one ? range - bound : bound;
         code = one ? code - bound : code;
-        *np = one ? prob - (prob >> kNumMoveBits) : prob + ((kBitModelTotal - prob) >> kNumMoveBits);
+        const uint32_t pv = vgpr(prob), m = 0u - vgpr(one ? 1u : 0u);   // a lane mask, not a branch
+        const uint32_t up = pv + ((kBitModelTotal - pv) >> kNumMoveBits), dn = pv - (pv >> kNumMoveBits);
+        *np = up ^ ((up ^ dn) & m);
         if (range < (1u << 24)) { code = (code << 8) | rd_byte(); range <<= 8; }
         return one ? 1u : 0u;
     }
