@@ -186,26 +186,25 @@ struct Dec {
         }
         return sym;
     }
-    // 256-node tree p[0..255] as two lane vectors of u32 pairs: nodes 2l, 2l+1 in lane l
-    // of lo (l < 64) / of hi (nodes 128 + ...). p is 4-byte aligned.
+    // 256-node tree p[0..255] as four lane vectors: node m in lane m % 64 of vector m / 64,
+    // so a walk's node read is one readlane with the node index (no half-word select)
+    struct T256 { uint32_t v[4][kVS]; };
     template <typename P>
-    DFI void fetch256(const P* p, uint32_t (&lo)[kVS], uint32_t (&hi)[kVS]) const {
-        const uint32_t* w = (const uint32_t*)p;
+    DFI void fetch256(const P* p, T256& t) const {
 #pragma unroll
-        for (int s = 0; s < kVS; s++) {
-            const uint32_t l = (uint32_t)(s * kWave) + lane;
-            lo[s] = w[l];
-            hi[s] = w[64 + l];
-        }
+        for (int k = 0; k < 4; k++)
+#pragma unroll
+            for (int s = 0; s < kVS; s++) t.v[k][s] = (uint32_t)p[64 * k + s * kWave + lane];
     }
-    DFI static uint32_t node256(const uint32_t (&lo)[kVS], const uint32_t (&hi)[kVS], uint32_t m) {
-        const uint32_t l = (m >> 1) & 63u;
-        const uint32_t w = (m & 128u) ? vget(hi, l) : vget(lo, l);
-        return (w >> ((m & 1u) << 4)) & 0xFFFFu;
+    // node m of tree level `level` (m in [2^level, 2^(level+1)))
+    DFI static uint32_t node256(const T256& t, uint32_t m, int level) {
+        if (level <= 5) return vget(t.v[0], m);
+        if (level == 6) return vget(t.v[1], m & 63u);
+        return (m & 64u) ? vget(t.v[3], m & 63u) : vget(t.v[2], m & 63u);
     }
     // Decoder.LenDecoder.Decode (Decoder.java:48-59) over prefetched nodes:
     // lv lanes 0-7 low[ps], 8-15 mid[ps], 16-17 the two choices; lo/hi the high tree
-    DFI void fetch_len(const uint16_t* L, uint32_t ps, uint32_t (&lv)[kVS], uint32_t (&lo)[kVS], uint32_t (&hi)[kVS]) const {
+    DFI void fetch_len(const uint16_t* L, uint32_t ps, uint32_t (&lv)[kVS], T256& ht) const {
 #pragma unroll
         for (int s = 0; s < kVS; s++) {
             const uint32_t m = (uint32_t)(s * kWave) + lane;
@@ -215,10 +214,9 @@ struct Dec {
             else if (m < 18) v = L[LEN_CHOICE + m - 16];
             lv[s] = v;
         }
-        fetch256(L + PL::HIGH, lo, hi);
+        fetch256(L + PL::HIGH, ht);
     }
-    DFI uint32_t len_dec(uint16_t* L, uint32_t ps, const uint32_t (&lv)[kVS], const uint32_t (&lo)[kVS],
-                         const uint32_t (&hi)[kVS]) {
+    DFI uint32_t len_dec(uint16_t* L, uint32_t ps, const uint32_t (&lv)[kVS], const T256& ht) {
         uint32_t np;
         uint32_t x = dbit(vget(lv, 16), &np);
         L[LEN_CHOICE] = (uint16_t)np;
@@ -242,7 +240,7 @@ struct Dec {
         }
 #pragma unroll
         for (int b = 0; b < 8; b++) {
-            const uint32_t prob = b < 7 ? (vget(lo, m >> 1) >> ((m & 1u) << 4)) & 0xFFFFu : node256(lo, hi, m);
+            const uint32_t prob = node256(ht, m, b);
             x = dbit(prob, &np);
             L[base + m] = (uint16_t)np;
             m = (m << 1) + x;
@@ -296,8 +294,9 @@ struct Dec {
             const bool matched = !st_is_char(state);
             const uint32_t mb = matched ? byte_back(now, rep0 + 1) : 0u;
             uint16_t* sub = lit + (size_t)(((now & ((1u << lp) - 1)) << lc) + (prev >> (8 - lc))) * 0x300;
-            uint32_t tlo[kVS], thi[kVS], mv[kVS];
-            fetch256(sub, tlo, thi);
+            T256 tt;
+            uint32_t mv[kVS];
+            fetch256(sub, tt);
 #pragma unroll
             for (int s = 0; s < kVS; s++) {
                 const uint32_t i = (uint32_t)(s * kWave) + lane;
@@ -321,8 +320,7 @@ struct Dec {
                     if (same) { idx = ((1 + mbit) << 8) + sym; prob = vget(mv, i); }
                     else {
                         idx = sym;
-                        if (i < 7) prob = (vget(tlo, sym >> 1) >> ((sym & 1u) << 4)) & 0xFFFFu;
-                        else prob = node256(tlo, thi, sym);
+                        prob = node256(tt, sym, (int)i);
                     }
                     const uint32_t x = dbit(prob, &np);
                     sub[idx] = (uint16_t)np;   // every lane, same address and value
@@ -336,9 +334,10 @@ struct Dec {
                 state = st_lit(state);
             } else {
                 uint32_t len;
-                uint32_t lv[kVS], lo[kVS], hi[kVS];
+                uint32_t lv[kVS];
+                T256 ht;
                 if (bit(probs + PL::IS_REP, state) == 1) {
-                    fetch_len(probs + PL::RLEN, ps, lv, lo, hi);
+                    fetch_len(probs + PL::RLEN, ps, lv, ht);
                     len = 0;
                     if (bit(probs + PL::G0, state) == 0) {
                         if (bit(probs + PL::R0L, (state << PBS) + ps) == 0) { state = st_short(state); len = 1; }
@@ -353,11 +352,11 @@ struct Dec {
                         rep1 = rep0;
                         rep0 = dist;
                     }
-                    if (len == 0) { len = len_dec(probs + PL::RLEN, ps, lv, lo, hi) + kMatchMinLen; state = st_long(state); }
+                    if (len == 0) { len = len_dec(probs + PL::RLEN, ps, lv, ht) + kMatchMinLen; state = st_long(state); }
                 } else {
-                    fetch_len(probs + PL::LEN, ps, lv, lo, hi);
+                    fetch_len(probs + PL::LEN, ps, lv, ht);
                     rep3 = rep2; rep2 = rep1; rep1 = rep0;
-                    len = kMatchMinLen + len_dec(probs + PL::LEN, ps, lv, lo, hi);
+                    len = kMatchMinLen + len_dec(probs + PL::LEN, ps, lv, ht);
                     state = st_match(state);
                     uint16_t* slot_p = probs + PL::PSLOT + (len_to_pos_state(len) << 6);
                     uint32_t sv[kVS], av[kVS];
