@@ -93,6 +93,44 @@ __global__ void __launch_bounds__(256) mf_prev_kernel(const uint32_t* __restrict
     prev[vals[i]] = (i > 0 && keys[i - 1] == k) ? vals[i - 1] : kNoPos;
 }
 
+// hash2 "last occurrence" (BinTree.java:183-193) without a sort: hash2 has only
+// 1024 values, so one wave sweeps its stream in position order with the heads in
+// LDS. Per round of 64 positions, one ballot per hash bit gives each lane the lanes
+// with its hash (wave-level multi-split); the nearest of them below the lane is its
+// predecessor, else the head, and the highest of them updates the head. Reads of
+// k2 and writes of prev2 are coalesced (position order).
+__global__ void __launch_bounds__(64) mf_prev2_kernel(const uint64_t* __restrict__ offs, const uint32_t* __restrict__ k2,
+                                                      uint32_t* __restrict__ prev2) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];   // dynamic LDS (the CPU emulation shares it)
+    uint32_t* head = (uint32_t*)smem;                                   // [1024]
+    const uint32_t lane = threadIdx.x;
+    for (uint32_t k = lane; k < 1024; k += 64) head[k] = kNoPos;
+    __syncthreads();
+    const uint32_t s = blockIdx.x;
+    const uint64_t lo = offs[s], n = offs[s + 1] - lo;
+    for (uint64_t r0 = 0; r0 < n; r0 += 64) {
+        const uint64_t i = r0 + lane;
+        const uint32_t key = i < n ? k2[lo + i] : kSentinel32;
+        const bool live = key != kSentinel32;   // sentinel: no insertion, no prev (as mf_prev_kernel)
+        const uint32_t d = key & 1023u;
+        uint64_t peers = __ballot(live);
+        for (int b = 0; b < 10; b++) {
+            const bool on = (d >> b) & 1u;
+            const uint64_t m = __ballot(on);
+            peers &= on ? m : ~m;
+        }
+        const uint64_t below = peers & ((1ull << lane) - 1);   // lane < 64
+        const uint64_t above = lane == 63 ? 0ull : (peers & ~((2ull << lane) - 1));
+        const uint32_t hd = live ? head[d] : kNoPos;
+        __builtin_amdgcn_wave_barrier();
+        if (live) {
+            prev2[lo + i] = below ? (uint32_t)(lo + r0) + (63u - (uint32_t)__builtin_clzll(below)) : hd;
+            if (above == 0) head[d] = (uint32_t)(lo + i);
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
 // chain heads of the hash4 sort. The sorts are segmented per stream, so each
 // stream's non-inserted tail (sentinel keys) ends its own segment; a sentinel run
 // is a chain of its own that mf_chain_len_kernel empties.
@@ -443,10 +481,9 @@ int run_match_finder(Ctx* ctx, const Derived& d, const uint8_t* in, const uint64
     if (bt4) {
         const unsigned prev_grid = (unsigned)(((total + B - 1) / B + 7) & ~7ull);   // total < 2^32: fits
         {
-            TimedLaunch tl(ctx, "mf_sort", st);
-            if ((rc = seg_radix_sort(ctx, false, w.k2, w.vals, w.ks, w.vs, w.son, w.son + total, w.hist, total, d_offs, nstreams, 10, st))) return rc;
+            TimedLaunch tl(ctx, "mf_prev2", st);
+            hipLaunchKernelGGL(mf_prev2_kernel, dim3(nstreams), dim3(64), 1024 * 4, st, d_offs, (const uint32_t*)w.k2, w.prev2);
         }
-        hipLaunchKernelGGL(mf_prev_kernel, dim3(prev_grid), dim3(B), 0, st, (const uint32_t*)w.ks, w.vs, total, w.prev2);
         {
             TimedLaunch tl(ctx, "mf_sort", st);
             if ((rc = seg_radix_sort(ctx, false, w.k3, w.vals, w.ks, w.vs, w.son, w.son + total, w.hist, total, d_offs, nstreams, 16, st))) return rc;
