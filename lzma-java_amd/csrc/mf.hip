@@ -108,9 +108,11 @@ __global__ void __launch_bounds__(64) mf_prev2_kernel(const uint64_t* __restrict
     __syncthreads();
     const uint32_t s = blockIdx.x;
     const uint64_t lo = offs[s], n = offs[s + 1] - lo;
+    uint32_t nkey = lane < n ? k2[lo + lane] : kSentinel32;   // the next round's key is loaded a round ahead
     for (uint64_t r0 = 0; r0 < n; r0 += 64) {
         const uint64_t i = r0 + lane;
-        const uint32_t key = i < n ? k2[lo + i] : kSentinel32;
+        const uint32_t key = nkey;
+        nkey = i + 64 < n ? k2[lo + i + 64] : kSentinel32;
         const bool live = key != kSentinel32;   // sentinel: no insertion, no prev (as mf_prev_kernel)
         const uint32_t d = key & 1023u;
         uint64_t peers = __ballot(live);

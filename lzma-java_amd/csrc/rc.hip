@@ -22,8 +22,8 @@
 //   * after each block the ring goes to HBM as 18 aligned dwords into the
 //     stream's own record region, which serves as the output staging area: a
 //     record is 2 bytes and makes at most one byte, so output position k is
-//     always far behind the records still to be read; rc_copy_kernel then
-//     copies each stream's bytes to the caller's output layout;
+//     always far behind the records still to be read; rc_merge_kernel then
+//     assembles each stream's bytes in the caller's output layout;
 //   * a pending run of two or more 0xFF bytes (cacheSize > 2 at an emission,
 //     about once per 2^16 shifts) only sets a flag: lanes that raised it replay
 //     the block from the saved state with the exact reference step, writing
@@ -112,14 +112,89 @@ __device__ __forceinline__ uint32_t rec_at(const uint32_t (&w)[32], int k) {
     return (w[k >> 1] >> ((k & 1) * 16)) & 0xFFFFu;
 }
 
-__global__ void __launch_bounds__(kRcLanes) rc_kernel(RcArgs a) {
-    __shared__ __attribute__((aligned(16))) uint32_t rings[kRcLanes * kRcStride / 4];
+// Segments: a stream's records are cut into kRcSegs runs at multiples of 128 records
+// (split_k = min(n, k * seglen)). The range sequence does not depend on low, so one
+// cheap range-only pass gives every segment its starting range; the segments are
+// then coded independently from low = 0 (8 lanes per stream), and rc_merge_kernel
+// adds them up. Why the sum is the reference's output: the coder's bytes are the
+// base-256 digits of low, a sum of bound contributions that normalisation shifts
+// by whole bytes; a segment started at the window of split_k with low = 0 produces
+// exactly its records' contributions, its cache byte at the digit before that
+// window. Segment k's bytes begin at pos_k, pos_{k+1} = pos_k + outlen_k + cs_k - 1
+// (emitted bytes + pending group = 1 + shifts), and its unfinished digits (cache,
+// cs_k - 1 pending 0xFF, the 4 bytes of low, the carry at the last pending digit)
+// add into the next segment's first bytes; carries run toward the stream start.
+// 128-record multiples: a segment's staged bytes (at most records + 1, plus the ring's
+// 72-byte write-back past them) then stay inside its own 2-byte-per-record region
+__device__ __forceinline__ uint64_t rc_seglen(uint64_t n) {
+    return ((n + 128 * kRcSegs - 1) / (128 * kRcSegs)) * 128;
+}
+__device__ __forceinline__ uint64_t rc_split(uint64_t n, uint64_t seglen, int k) {
+    const uint64_t v = (uint64_t)k * seglen;
+    return v < n ? v : n;
+}
+
+// range-only pass: seg[s][k].range for k = 1 .. kRcSegs - 1, one lane per stream
+__global__ void __launch_bounds__(kRcLanes) rc_range_kernel(RcArgs a) {
     const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x);
     if (i >= a.nstreams) return;
     const uint32_t s = a.order[i];
     if (a.status[s] != LZMA_OK) return;
-    const uint64_t n = a.rec_lens[s];
-    uint16_t* region = a.recs + a.rec_offs[s];   // 64-record (128-byte) aligned
+    const uint64_t n = a.rec_lens[s], seglen = rc_seglen(n);
+    const uint32_t* r32 = (const uint32_t*)(a.recs + a.rec_offs[s]);
+    uint32_t* seg = a.seg + (size_t)s * kRcSegs * kRcSegWords;
+    const uint64_t need = rc_split(n, seglen, kRcSegs - 1);   // records before the last split
+    uint32_t range = 0xFFFFFFFFu;
+    seg[0] = range;
+    int next = 1;                                            // next split to record
+    auto step = [&](uint32_t rec) {   // Encode / EncodeDirectBits, range only
+        const uint32_t p = rec & 0x7FFu;
+        const bool bit = (rec & 0x800u) != 0, direct = p == 0;
+        const uint32_t bp = (range >> 11) * p, bd = range >> 1;
+        const uint32_t bound = direct ? bd : bp;
+        const uint32_t r1 = (bit && !direct) ? range - bp : bound;
+        range = r1 < (1u << 24) ? r1 << 8 : r1;
+    };
+    const uint64_t nblk = (need + 63) >> 6, full = need >> 6;
+    uint32_t cur[32], nxt[32];
+    if (nblk) {
+#pragma unroll
+        for (int j = 0; j < 32; j++) cur[j] = __builtin_nontemporal_load(r32 + j);
+    }
+    for (uint64_t b = 0; b < nblk; b++) {
+        while (next < kRcSegs && rc_split(n, seglen, next) == b * 64) seg[(next++) * kRcSegWords] = range;
+        if (b + 1 < nblk) {
+#pragma unroll
+            for (int j = 0; j < 32; j++) nxt[j] = __builtin_nontemporal_load(r32 + (b + 1) * 32 + j);
+        }
+        if (b < full) {
+#pragma unroll
+            for (int k = 0; k < 64; k++) step(rec_at(cur, k));
+        } else {
+            const uint32_t m = (uint32_t)(need & 63);
+#pragma unroll 1
+            for (uint32_t k = 0; k < m; k++) step(rec_at(cur, (int)k));
+        }
+#pragma unroll
+        for (int j = 0; j < 32; j++) cur[j] = nxt[j];
+    }
+    while (next < kRcSegs) seg[(next++) * kRcSegWords] = range;   // splits at `need` (and empty segments)
+}
+
+// one lane per (stream, segment): the segment's records from its starting range and
+// low = 0; bytes staged at the segment's own record offset, state left in seg[s][k]
+__global__ void __launch_bounds__(kRcLanes) rc_kernel(RcArgs a) {
+    __shared__ __attribute__((aligned(16))) uint32_t rings[kRcLanes * kRcStride / 4];
+    const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (i >= a.nstreams * kRcSegs) return;
+    const uint32_t s = a.order[i / kRcSegs];
+    const int sk = i % kRcSegs;
+    if (a.status[s] != LZMA_OK) return;
+    const uint64_t nall = a.rec_lens[s], seglen = rc_seglen(nall);
+    const uint64_t r0 = rc_split(nall, seglen, sk);
+    const uint64_t n = (sk + 1 < kRcSegs ? rc_split(nall, seglen, sk + 1) : nall) - r0;
+    uint16_t* region = a.recs + a.rec_offs[s] + r0;   // 64-record (128-byte) aligned
+    uint32_t* seg = a.seg + ((size_t)s * kRcSegs + sk) * kRcSegWords;
     const uint32_t* r32 = (const uint32_t*)region;
     uint32_t* ring32 = rings + threadIdx.x * (kRcStride / 4);
     uint32_t* stage32 = (uint32_t*)region;
@@ -128,7 +203,7 @@ __global__ void __launch_bounds__(kRcLanes) rc_kernel(RcArgs a) {
     c.ring = (uint8_t*)ring32;
     c.outpos = 0;
     c.tailw = 0;
-    c.lo = 0; c.carry = 0; c.range = 0xFFFFFFFFu; c.cache = 0; c.cache_size = 1;   // Init (:18-24)
+    c.lo = 0; c.carry = 0; c.range = seg[0]; c.cache = 0; c.cache_size = 1;   // Init (:18-24) at the segment's range
     // blocks of 64 records (32 dwords per lane); the next block's loads are issued
     // before this block is coded, so their HBM latency overlaps the coding
     const uint64_t nblk = (n + 63) >> 6, full = n >> 6;
@@ -174,32 +249,77 @@ __global__ void __launch_bounds__(kRcLanes) rc_kernel(RcArgs a) {
 #pragma unroll
         for (int j = 0; j < 32; j++) cur[j] = nxt[j];
     }
+    if (sk == kRcSegs - 1) {
 #pragma unroll 1
-    for (int k = 0; k < 5; k++) c.shift_low();   // FlushData (:31-36)
-    const uint64_t cap = a.out_offs[s + 1] - a.out_offs[s];
-    a.out_lens[s] = c.outpos;
-    if (c.outpos > cap) a.status[s] = LZMA_E_OVERFLOW;
+        for (int k = 0; k < 5; k++) c.shift_low();   // FlushData (:31-36)
+    }
+    seg[1] = c.outpos; seg[2] = c.lo; seg[3] = c.carry; seg[4] = c.cache; seg[5] = c.cache_size;
 }
 
-// staged bytes of each stream to the caller's output layout: one block per stream
-__global__ void __launch_bounds__(256) rc_copy_kernel(RcArgs a) {
+// the segments of a stream into the caller's output layout (one workgroup per stream):
+// emitted bytes copied in parallel, then thread 0 adds each segment's unfinished digits
+// into the next segment's first bytes, carries running toward the stream start
+__global__ void __launch_bounds__(256) rc_merge_kernel(RcArgs a) {
     const uint32_t s = blockIdx.x;
     if (a.status[s] != LZMA_OK) return;
-    const uint8_t* src = (const uint8_t*)(a.recs + a.rec_offs[s]);
+    const uint32_t* seg = a.seg + (size_t)s * kRcSegs * kRcSegWords;
+    const uint64_t nall = a.rec_lens[s], seglen = rc_seglen(nall);
+    uint64_t pos[kRcSegs + 1];
+    pos[0] = 0;
+    for (int k = 0; k < kRcSegs; k++) {
+        const uint32_t* g = seg + k * kRcSegWords;
+        pos[k + 1] = pos[k] + g[1] + g[5] - 1;
+    }
+    const uint64_t total = pos[kRcSegs - 1] + seg[(kRcSegs - 1) * kRcSegWords + 1];
+    const uint64_t cap = a.out_offs[s + 1] - a.out_offs[s];
+    if (threadIdx.x == 0) a.out_lens[s] = total;
+    if (total > cap) {
+        if (threadIdx.x == 0) a.status[s] = LZMA_E_OVERFLOW;
+        return;
+    }
     uint8_t* dst = a.out + a.out_offs[s];
-    const uint64_t len = a.out_lens[s];
-    for (uint64_t k = threadIdx.x; k < len; k += blockDim.x) dst[k] = src[k];
+    for (int k = 0; k < kRcSegs; k++) {
+        const uint8_t* src = (const uint8_t*)(a.recs + a.rec_offs[s] + rc_split(nall, seglen, k));
+        const uint32_t len = seg[k * kRcSegWords + 1];
+        const uint64_t end = k + 1 < kRcSegs ? pos[k + 1] : total;   // the pending digits start as 0
+        for (uint64_t j = threadIdx.x; j < end - pos[k]; j += blockDim.x) dst[pos[k] + j] = j < len ? src[j] : 0;
+    }
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    for (int k = 0; k + 1 < kRcSegs; k++) {
+        const uint32_t* g = seg + k * kRcSegWords;
+        const uint32_t len = g[1], lo = g[2], cy = g[3], cache = g[4], cs = g[5];
+        const uint64_t q0 = pos[k] + len;   // the cache digit
+        // digits of the unfinished part, least significant first: low's 4 bytes, then the
+        // pending group (cs - 1 x 0xFF, the cache) with the coder's carry at its last digit
+        uint32_t carry = 0;
+        for (int t = (int)cs + 3; t >= 0; t--) {
+            const uint64_t q = q0 + (uint64_t)t;
+            uint32_t d;
+            if (t >= (int)cs) d = (lo >> (8 * (3 - (t - (int)cs)))) & 0xFFu;
+            else d = t == 0 ? cache : 0xFFu;
+            if (t == (int)cs - 1) d += cy;
+            const uint32_t v = (uint32_t)dst[q] + d + carry;
+            dst[q] = (uint8_t)v;
+            carry = v >> 8;
+        }
+        for (uint64_t q = q0; carry && q > 0;) {   // rare: through earlier 0xFF digits
+            q--;
+            const uint32_t v = (uint32_t)dst[q] + carry;
+            dst[q] = (uint8_t)v;
+            carry = v >> 8;
+        }
+    }
 }
 
 int launch_rc(Ctx* ctx, const RcArgs& a, hipStream_t st) {
     if (a.nstreams <= 0) return LZMA_OK;
     {
         TimedLaunch tl(ctx, "enc_rc", st);
-        hipLaunchKernelGGL(rc_kernel, dim3((a.nstreams + kRcLanes - 1) / kRcLanes), dim3(kRcLanes), 0, st, a);
-    }
-    {
-        TimedLaunch tl(ctx, "enc_rc_copy", st);
-        hipLaunchKernelGGL(rc_copy_kernel, dim3(a.nstreams), dim3(256), 0, st, a);
+        hipLaunchKernelGGL(rc_range_kernel, dim3((a.nstreams + kRcLanes - 1) / kRcLanes), dim3(kRcLanes), 0, st, a);
+        const int lanes = a.nstreams * kRcSegs;
+        hipLaunchKernelGGL(rc_kernel, dim3((lanes + kRcLanes - 1) / kRcLanes), dim3(kRcLanes), 0, st, a);
+        hipLaunchKernelGGL(rc_merge_kernel, dim3(a.nstreams), dim3(256), 0, st, a);
     }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return ctx->fail(LZMA_E_DEVICE, "rc launch: %s", hipGetErrorString(e));

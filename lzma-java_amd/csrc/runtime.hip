@@ -153,6 +153,7 @@ static int encode_pass(Ctx* ctx, const Derived& d, const uint8_t* d_in, const ui
         const size_t union_bytes = std::max<size_t>(p1_bytes, rofs[ns] * 2);
         uint16_t* d_recs = nullptr;
         uint64_t *d_rofs = nullptr, *d_rlens = nullptr;
+        uint32_t* d_seg = nullptr;
         auto need = [&](Carver& c, MfBuffers& w, uint8_t** inpad, uint64_t** d_offs, uint64_t** d_oofs,
                         uint32_t** d_order, uint64_t** d_lens, int32_t** d_status, unsigned** d_next, uint8_t** d_scr) {
             *inpad = c.take<uint8_t>(T + 512);
@@ -164,6 +165,7 @@ static int encode_pass(Ctx* ctx, const Derived& d, const uint8_t* d_in, const ui
             *d_next = c.take<unsigned>(4);
             d_rofs = c.take<uint64_t>(ns + 1);
             d_rlens = c.take<uint64_t>(ns);
+            d_seg = c.take<uint32_t>((size_t)ns * kRcSegs * kRcSegWords);
             uint8_t* u = c.take<uint8_t>(union_bytes);
             d_recs = (uint16_t*)u;
             Carver c1(u);
@@ -254,7 +256,7 @@ static int encode_pass(Ctx* ctx, const Derived& d, const uint8_t* d_in, const ui
         watch.stop();
         RcArgs ra{};
         ra.recs = d_recs; ra.rec_offs = d_rofs; ra.rec_lens = d_rlens; ra.order = d_order; ra.nstreams = ns;
-        ra.status = d_status; ra.out = d_out; ra.out_offs = d_oofs; ra.out_lens = d_lens;
+        ra.status = d_status; ra.out = d_out; ra.out_offs = d_oofs; ra.out_lens = d_lens; ra.seg = d_seg;
         if ((rc = launch_rc(ctx, ra, st))) return rc;
         LZG_TRACE(ctx, st, "enc_rc done");
 #ifdef LZG_PROF
