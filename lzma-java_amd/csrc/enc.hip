@@ -35,7 +35,8 @@ namespace lzg {
 
 static __constant__ Tables c_tab = make_tables();
 
-constexpr int kOptLds = 64;         // _optimum slots kept in LDS (deeper slots spill to HBM)
+constexpr int kOptLds = 64;         // _optimum slots kept in LDS (deeper slots spill to HBM); the LDS arrays
+                                    // have one more slot, kOptLds, a sink for the writes of idle lanes
 constexpr int kLitLdsMaxBits = 1;   // literal coders in LDS when lc + lp <= 1 (<= 3 KiB); else HBM/L2
 constexpr int kMdCap = kMatchMaxLen + 1;
 constexpr int kRing = 32;           // match-info prefetch window (positions)
@@ -257,18 +258,26 @@ struct Enc {
             uint32_t diff = (mb ^ sym) & 0xFFu;
             first = diff ? 31 - __clz(diff) : -1;
         }
+#if LZG_WAVE == 64
+        {   // every lane computes bit (lane & 7): no exec-mask bookkeeping on the scalar unit;
+            // lanes 8-63 repeat lanes 0-7's addresses and their prices are dropped
+            const int i = 7 - (int)(lane & 7u);
+            const uint32_t bit = (sym >> i) & 1;
+            const uint32_t ctx = (0x100u | sym) >> (i + 1);
+            const uint32_t idx = (match_mode && i >= first) ? ((1 + ((mb >> i) & 1)) << 8) + ctx : ctx;
+            const uint32_t pr = price_bit(p[idx], bit);
+            price = lane < 8 ? pr : 0u;
+        }
+#else
         LANE_FOR(int, j, 0, 8) {
             int i = 7 - j;
             uint32_t bit = (sym >> i) & 1;
             uint32_t ctx = (0x100u | sym) >> (i + 1);
             uint32_t idx = ctx;
             if (match_mode && i >= first) idx = ((1 + ((mb >> i) & 1)) << 8) + ctx;
-#ifdef LZG_ABL_LITLOAD
-            price += price_bit(1024u + (idx & 7u), bit);   // ablation: no literal-model load
-#else
             price += price_bit(p[idx], bit);
-#endif
         }
+#endif
 #if LZG_WAVE == 64
         // sum of lanes 0-7 without LDS traffic: DPP quad swaps, then a rotate by 4
         // within the 16-lane row; lane 0 holds the total (readlane keeps it scalar)
@@ -423,8 +432,12 @@ struct Enc {
     // one decision against probs[index]
     FI void q_bit(Q& q, uint32_t index, uint32_t bit) const {
 #pragma unroll
-        for (int t = 0; t < kQS; t++)
-            if ((uint32_t)(t * kWave) + lane == q.n) { q.idx[t] = index; q.bit[t] = bit; q.kind[t] = QK_PROB; }
+        for (int t = 0; t < kQS; t++) {   // selects, not a branch: the exec-mask juggling runs on the scalar unit
+            const bool m = (uint32_t)(t * kWave) + lane == q.n;
+            q.idx[t] = m ? index : q.idx[t];
+            q.bit[t] = m ? bit : q.bit[t];
+            q.kind[t] = m ? (uint32_t)QK_PROB : q.kind[t];
+        }
         q.n++;
     }
     // BitTreeEncoder.Encode (BitTreeEncoder.java:18-27): node of bit i (MSB first) = the i-bit prefix
@@ -432,11 +445,11 @@ struct Enc {
 #pragma unroll
         for (int t = 0; t < kQS; t++) {
             const uint32_t i = (uint32_t)(t * kWave) + lane - q.n;
-            if (i < nbits) {
-                q.idx[t] = base + ((sym | (1u << nbits)) >> (nbits - i));
-                q.bit[t] = (sym >> (nbits - 1 - i)) & 1u;
-                q.kind[t] = QK_PROB;
-            }
+            const bool m = i < nbits;
+            const uint32_t ic = m ? i : 0u;
+            q.idx[t] = m ? base + ((sym | (1u << nbits)) >> (nbits - ic)) : q.idx[t];
+            q.bit[t] = m ? (sym >> (nbits - 1 - ic)) & 1u : q.bit[t];
+            q.kind[t] = m ? (uint32_t)QK_PROB : q.kind[t];
         }
         q.n += nbits;
     }
@@ -446,12 +459,12 @@ struct Enc {
 #pragma unroll
         for (int t = 0; t < kQS; t++) {
             const uint32_t i = (uint32_t)(t * kWave) + lane - q.n;
-            if (i < nbits) {
-                const uint32_t m = (1u << i) | (i ? brev32(sym) >> (32 - i) : 0u);
-                q.idx[t] = base + m;
-                q.bit[t] = (sym >> i) & 1u;
-                q.kind[t] = QK_PROB;
-            }
+            const bool in = i < nbits;
+            const uint32_t ic = in ? i : 0u;
+            const uint32_t m = (1u << ic) | (ic ? brev32(sym) >> (32 - ic) : 0u);
+            q.idx[t] = in ? base + m : q.idx[t];
+            q.bit[t] = in ? (sym >> ic) & 1u : q.bit[t];
+            q.kind[t] = in ? (uint32_t)QK_PROB : q.kind[t];
         }
         q.n += nbits;
     }
@@ -460,7 +473,9 @@ struct Enc {
 #pragma unroll
         for (int t = 0; t < kQS; t++) {
             const uint32_t i = (uint32_t)(t * kWave) + lane - q.n;
-            if (i < nbits) { q.bit[t] = (v >> (nbits - 1 - i)) & 1u; q.kind[t] = QK_DIRECT; }
+            const bool m = i < nbits;
+            q.bit[t] = m ? (v >> (nbits - 1 - (m ? i : 0u))) & 1u : q.bit[t];
+            q.kind[t] = m ? (uint32_t)QK_DIRECT : q.kind[t];
         }
         q.n += nbits;
     }
@@ -475,13 +490,12 @@ struct Enc {
 #pragma unroll
         for (int t = 0; t < kQS; t++) {
             const uint32_t j = (uint32_t)(t * kWave) + lane - q.n;
-            if (j < 8u) {
-                const int i = 7 - (int)j;
-                const uint32_t ctx = (0x100u | sym) >> (i + 1);
-                q.idx[t] = base + ((matched && i >= first) ? ((1 + ((mb >> i) & 1)) << 8) + ctx : ctx);
-                q.bit[t] = (sym >> i) & 1u;
-                q.kind[t] = QK_LIT;
-            }
+            const bool m = j < 8u;
+            const int i = 7 - (int)(j & 7u);
+            const uint32_t ctx = (0x100u | sym) >> (i + 1);
+            q.idx[t] = m ? base + ((matched && i >= first) ? ((1 + ((mb >> i) & 1)) << 8) + ctx : ctx) : q.idx[t];
+            q.bit[t] = m ? (sym >> i) & 1u : q.bit[t];
+            q.kind[t] = m ? (uint32_t)QK_LIT : q.kind[t];
         }
         q.n += 8;
     }
@@ -497,29 +511,33 @@ struct Enc {
         }
     }
     FI void q_run(const Q& q) {
+        // branch-free: every lane loads and stores; lanes whose slot is not of a kind use the
+        // sink entry past that table (lit: nlit, probs: E_COUNT, dmp: E_PSLOT, rbuf: kRbuf)
+        const uint32_t nlit = 0x300u << (lc + lp);
         uint32_t pr[kQS];
 #pragma unroll
         for (int t = 0; t < kQS; t++) {
-            pr[t] = 0;
-            if (q.kind[t] == QK_LIT) pr[t] = lit[q.idx[t]];
-            else if (q.kind[t] == QK_PROB) pr[t] = probs[q.idx[t]];
+            const bool isl = q.kind[t] == QK_LIT, isp = q.kind[t] == QK_PROB;
+            const uint32_t lv = lit[isl ? q.idx[t] : nlit];
+            const uint32_t pv = probs[isp ? q.idx[t] : (uint32_t)E_COUNT];
+            pr[t] = isl ? lv : (isp ? pv : 0u);
         }
         const uint32_t base = (uint32_t)rpos;
 #pragma unroll
         for (int t = 0; t < kQS; t++) {
             const uint32_t j = (uint32_t)(t * kWave) + lane;
-            if (j < q.n) rbuf[(base + j) & (kRbuf - 1)] = (uint16_t)((q.kind[t] == QK_DIRECT ? 0u : pr[t]) | (q.bit[t] << 11));
+            const bool isl = q.kind[t] == QK_LIT, isp = q.kind[t] == QK_PROB;
+            rbuf[j < q.n ? (base + j) & (kRbuf - 1) : (uint32_t)kRbuf] =
+                (uint16_t)((q.kind[t] == QK_DIRECT ? 0u : pr[t]) | (q.bit[t] << 11));
             const uint32_t p = pr[t];
             const uint16_t np = (uint16_t)(q.bit[t] ? p - (p >> kNumMoveBits) : p + ((kBitModelTotal - p) >> kNumMoveBits));
 #ifdef LZG_ABL_LITSTORE
-            if (q.kind[t] == QK_LIT) {}   // ablation: literal models never adapt
+            lit[nlit] = np;   // ablation: literal models never adapt
 #else
-            if (q.kind[t] == QK_LIT) lit[q.idx[t]] = np;
+            lit[isl ? q.idx[t] : nlit] = np;
 #endif
-            else if (q.kind[t] == QK_PROB) {
-                probs[q.idx[t]] = np;
-                if (q.idx[t] < (uint32_t)E_PSLOT) dmp[q.idx[t]] = price0(np) | (price1(np) << 16);
-            }
+            probs[isp ? q.idx[t] : (uint32_t)E_COUNT] = np;
+            dmp[(isp && q.idx[t] < (uint32_t)E_PSLOT) ? q.idx[t] : (uint32_t)E_PSLOT] = price0(np) | (price1(np) << 16);
         }
         LANE_FENCE();
         const uint64_t p0 = rpos;
@@ -652,8 +670,11 @@ struct Enc {
     // while (lenEnd < target) _optimum[++lenEnd].Price = kIfinityPrice
     FI void extend_to(uint32_t& len_end, uint32_t target) {
         if (len_end >= target) return;
-        if (target < (uint32_t)kOptLds) {
-            LANE_FOR(uint32_t, i, len_end + 1, target + 1) set_price<true>(i, kInfinityPrice);
+        if (target < (uint32_t)kOptLds) {   // branch-free: idle lanes write the sink slot
+            for (uint32_t i0 = len_end + 1; i0 <= target; i0 += kWave) {
+                const uint32_t i = i0 + lane;
+                o_price[i <= target ? i : (uint32_t)kOptLds] = kInfinityPrice;
+            }
             len_end = target;
             LANE_FENCE();
             return;
@@ -666,14 +687,18 @@ struct Enc {
     FI void relax_rep(uint32_t base_slot, uint32_t lo, uint32_t hi, uint32_t price_base, uint32_t ps,
                       uint32_t pos_prev_v, uint32_t ri) {
         if (base_slot + hi < (uint32_t)kOptLds) {   // all slots in LDS: no per-lane spill branches
-            LANE_FOR(uint32_t, l, lo, hi + 1) {
-                const uint32_t cl = price_base + len_price(1, l - 2, ps), s = base_slot + l;
-                if (cl < o_price[s]) {
-                    o_price[s] = cl;
-                    o_pp[s] = (o_pp[s] & 0xFFFF0000u) | pos_prev_v;
-                    o_bp[s] = (int32_t)ri;
-                    o_fs[s] = (uint8_t)(o_fs[s] & ~1u);
-                }
+            // branch-free: idle lanes and lanes that do not improve write the sink slot
+            for (uint32_t l0 = lo; l0 <= hi; l0 += kWave) {
+                const uint32_t l = l0 + lane;
+                const bool ok = l <= hi;
+                const uint32_t s = ok ? base_slot + l : (uint32_t)kOptLds;
+                const uint32_t cl = price_base + len_price(1, ok ? l - 2 : 0u, ps);
+                const uint32_t op = o_price[s], opp = o_pp[s], ofs = o_fs[s];
+                const uint32_t t = (ok && cl < op) ? s : (uint32_t)kOptLds;
+                o_price[t] = cl;
+                o_pp[t] = (opp & 0xFFFF0000u) | pos_prev_v;
+                o_bp[t] = (int32_t)ri;
+                o_fs[t] = (uint8_t)(ofs & ~1u);
             }
             LANE_FENCE();
             return;
@@ -693,15 +718,18 @@ struct Enc {
     // lanes relax slots base+l, l in [lo, hi], all with the match distance `dist`
     FI void relax_match(uint32_t base_slot, uint32_t lo, uint32_t hi, uint32_t price_base, uint32_t dist, uint32_t ps,
                         uint32_t pos_prev_v) {
-        if (base_slot + hi < (uint32_t)kOptLds) {   // all slots in LDS
-            LANE_FOR(uint32_t, l, lo, hi + 1) {
-                const uint32_t cl = price_base + pos_len_price(dist, l, ps), s = base_slot + l;
-                if (cl < o_price[s]) {
-                    o_price[s] = cl;
-                    o_pp[s] = (o_pp[s] & 0xFFFF0000u) | pos_prev_v;
-                    o_bp[s] = (int32_t)(dist + kNumRepDistances);
-                    o_fs[s] = (uint8_t)(o_fs[s] & ~1u);
-                }
+        if (base_slot + hi < (uint32_t)kOptLds) {   // all slots in LDS; branch-free as relax_rep
+            for (uint32_t l0 = lo; l0 <= hi; l0 += kWave) {
+                const uint32_t l = l0 + lane;
+                const bool ok = l <= hi;
+                const uint32_t s = ok ? base_slot + l : (uint32_t)kOptLds;
+                const uint32_t cl = price_base + pos_len_price(dist, ok ? l : (uint32_t)kMatchMinLen, ps);
+                const uint32_t op = o_price[s], opp = o_pp[s], ofs = o_fs[s];
+                const uint32_t t = (ok && cl < op) ? s : (uint32_t)kOptLds;
+                o_price[t] = cl;
+                o_pp[t] = (opp & 0xFFFF0000u) | pos_prev_v;
+                o_bp[t] = (int32_t)(dist + kNumRepDistances);
+                o_fs[t] = (uint8_t)(ofs & ~1u);
             }
             LANE_FENCE();
             return;
@@ -1279,10 +1307,10 @@ enum { L_PP, L_PROBS, L_DMP, L_LENP, L_LENC, L_PSP, L_DP, L_AP, L_TP, L_MDLEN, L
 __host__ __device__ inline uint32_t enc_lds_layout(const EncArgs& a, uint32_t* off) {
     const uint32_t md_cap = a.fb + 2;   // pairs per position <= fb (+1 clamp slot)
     const uint32_t sz[L_COUNT] = {
-        512 * 2, prob_count(a.pb) * 2, dm_count(a.pb) * 4, 2 * (1u << a.pb) * a.len_table_size * 2, 2 * 16 * 4, 256 * 2, 512 * 2, 16 * 4,
-        0u /* tp aliases the gather window */, md_cap * 2, md_cap * 4, kRing * 4, kRing * kInlinePairs * a.pair_bytes, kOptLds * 4, kOptLds * 4,
-        kOptLds * 4, kOptLds * 4, kOptLds, 4 * kOptLds * 4, kOptLds * 4, kSides * kGW, kRbuf * 2,
-        a.lit_in_lds ? (0x300u << (a.lc + a.lp)) * 2 : 0u};
+        512 * 2, prob_count(a.pb) * 2 + 2, dm_count(a.pb) * 4 + 4, 2 * (1u << a.pb) * a.len_table_size * 2, 2 * 16 * 4, 256 * 2, 512 * 2, 16 * 4,
+        0u /* tp aliases the gather window */, md_cap * 2, md_cap * 4, kRing * 4, kRing * kInlinePairs * a.pair_bytes,
+        (kOptLds + 1) * 4, (kOptLds + 1) * 4, (kOptLds + 1) * 4, kOptLds * 4, kOptLds + 1, 4 * kOptLds * 4, kOptLds * 4, kSides * kGW, kRbuf * 2 + 2,
+        a.lit_in_lds ? (0x300u << (a.lc + a.lp)) * 2 + 2 : 0u};
     uint32_t o = 0;
     for (int i = 0; i < L_COUNT; i++) { if (off) off[i] = o; o += (sz[i] + 15) & ~15u; }
     return o;
@@ -1388,7 +1416,7 @@ size_t enc_lds_bytes(const EncArgs& a) { return enc_lds_layout(a, nullptr); }
 
 size_t enc_scratch_per_block(const Derived&) { return (size_t)kNumOpts * 4 * 10 + 256; }
 
-size_t enc_lit_bytes(const Derived& d) { return ((size_t)0x300 << (d.lc + d.lp)) * 2; }
+size_t enc_lit_bytes(const Derived& d) { return ((size_t)0x300 << (d.lc + d.lp)) * 2 + 2; }   // + the sink entry
 
 uint32_t enc_lit_in_lds(const Derived& d) { return (d.lc + d.lp) <= (uint32_t)kLitLdsMaxBits; }
 

@@ -197,6 +197,11 @@ inline T __shfl(T v, int src, int width = 64) {
     return out;
 }
 template <typename T>
+inline T __shfl_up(T v, unsigned delta, int width = 64) {
+    const unsigned l = threadIdx.x & 63u;
+    return __shfl(v, (int)(l >= delta ? l - delta : l), width);
+}
+template <typename T>
 inline T __shfl_xor(T v, int mask, int width = 64) {
     return __shfl(v, (int)((threadIdx.x & 63u) ^ (unsigned)mask), width);
 }
