@@ -265,7 +265,7 @@ struct RcArgs {
     uint64_t* out_lens;
     uint32_t* seg;                // [nstreams][kRcSegs][kRcSegWords]: start range, bytes, lo, carry, cache, cache size
 };
-constexpr int kRcSegs = 8;        // coder segments per stream (rc.hip)
+constexpr int kRcSegs = 16;       // coder segments per stream (rc.hip)
 constexpr int kRcSegWords = 8;
 int launch_rc(Ctx* ctx, const RcArgs& a, hipStream_t st);
 // records one stream of n bytes can need: <= 21 per byte (a length-2 match: isMatch, isRep,
