@@ -147,13 +147,19 @@ __global__ void __launch_bounds__(kRcLanes) rc_range_kernel(RcArgs a) {
     uint32_t range = 0xFFFFFFFFu;
     seg[0] = range;
     int next = 1;                                            // next split to record
-    auto step = [&](uint32_t rec) {   // Encode / EncodeDirectBits, range only
+    // Encode / EncodeDirectBits, range only. bit ? range - t*p : t*p (t = range >> 11) is one
+    // 24-bit multiply-add, (range & -bit) + t * (bit ? -p : p), exact mod 2^32; the next range
+    // is >= 2^17 (t >= 2^13, 31 <= p <= 2017), so it needs the 8-bit shift exactly when its
+    // leading-zero count has bit 3 set (8..14)
+    auto step = [&](uint32_t rec) {
         const uint32_t p = rec & 0x7FFu;
-        const bool bit = (rec & 0x800u) != 0, direct = p == 0;
-        const uint32_t bp = (range >> 11) * p, bd = range >> 1;
-        const uint32_t bound = direct ? bd : bp;
-        const uint32_t r1 = (bit && !direct) ? range - bp : bound;
-        range = r1 < (1u << 24) ? r1 << 8 : r1;
+        const uint32_t bm = 0u - ((rec >> 11) & 1u);
+        const int32_t q = (int32_t)((p ^ bm) - bm);
+        const uint32_t t = range >> 11;
+        const uint32_t r1p = (range & bm) + (uint32_t)((int32_t)t * q);
+        const uint32_t dm = 0u - (uint32_t)(p == 0);   // a direct bit: range >> 1 (a mask, not a branch)
+        const uint32_t r1 = r1p ^ ((r1p ^ (range >> 1)) & dm);
+        range = r1 << ((uint32_t)__builtin_clz(r1) & 8u);
     };
     const uint64_t nblk = (need + 63) >> 6, full = need >> 6;
     uint32_t cur[32], nxt[32];
