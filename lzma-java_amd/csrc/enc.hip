@@ -749,6 +749,27 @@ struct Enc {
     // getOptimum's match candidates of position 0 (Encoder.java:620-640)
     template <bool F>
     FI void relax_first(uint32_t lstart, uint32_t len_main, uint32_t npairs, uint32_t normal_match_price, uint32_t pos_state) {
+        if (F) {   // all slots in LDS: branch-free (idle and non-improving lanes write the sink slot)
+            for (uint32_t l0 = lstart; l0 <= len_main; l0 += kWave) {
+                const uint32_t l = l0 + lane;
+                const bool ok = l <= len_main;
+                // the pair of length l: the first with md_len >= l (lengths increase), i.e. the count of
+                // shorter ones among the first npairs - 1 -- a uniform loop instead of a per-lane while
+                uint32_t k = 0;
+                for (uint32_t kk = 0; kk + 1 < npairs; kk++) k += l > md_len[kk] ? 1u : 0u;
+                const uint32_t distance = md_dist[k];
+                const uint32_t s = ok ? l : (uint32_t)kOptLds;
+                const uint32_t cl = normal_match_price + pos_len_price(distance, ok ? l : (uint32_t)kMatchMinLen, pos_state);
+                const uint32_t op = o_price[s], opp = o_pp[s], ofs = o_fs[s];
+                const uint32_t t = (ok && cl < op) ? s : (uint32_t)kOptLds;
+                o_price[t] = cl;
+                o_pp[t] = opp & 0xFFFF0000u;
+                o_bp[t] = (int32_t)(distance + kNumRepDistances);
+                o_fs[t] = (uint8_t)(ofs & ~1u);
+            }
+            LANE_FENCE();
+            return;
+        }
         LANE_FOR(uint32_t, l, lstart, len_main + 1) {
             uint32_t k = 0;
             while (k + 1 < npairs && l > md_len[k]) k++;
