@@ -249,18 +249,24 @@ struct Dec {
     }
     // OutWindow.CopyBlock (OutWindow.java:53-67) of len bytes at distance d1,
     // byte-serial semantics: an overlapping copy repeats the d1-byte period.
-    DFI void copy(uint32_t now, uint32_t d1, uint32_t len) {
+    // Returns the byte one past the copy, out[now + len - d1]: the match byte of a literal
+    // that follows (Decoder.java:85, GetByte(rep0)), fetched in the copy's own round trip.
+    DFI uint32_t copy(uint32_t now, uint32_t d1, uint32_t len) {
         LANE_FENCE();
-        for (uint32_t k0 = 0; k0 < len; k0 += kWave) {
+        uint32_t next = 0;
+        for (uint32_t k0 = 0; k0 <= len; k0 += kWave) {
             const uint32_t k = k0 + lane;
-            if (k < len) {
+            if (k <= len) {
                 // source = now - d1 + (k mod d1): always before `now`, so lanes never
                 // read a byte this copy writes (and kNear + 273 < kWin: no ring alias)
                 const uint32_t r = d1 > len ? k : k % d1;
-                win[(now + k) & (kWin - 1)] = (uint8_t)byte_back(now, d1 - r);
+                const uint32_t v = byte_back(now, d1 - r);
+                if (k < len) win[(now + k) & (kWin - 1)] = (uint8_t)v;
+                else next = v;
             }
         }
         LANE_FENCE();
+        return (uint32_t)__builtin_amdgcn_readlane((int)next, (int)(len % kWave));
     }
 
     // returns LZMA_OK / LZMA_E_DATA / LZMA_E_OVERFLOW; *now_out = bytes written
@@ -279,6 +285,7 @@ struct Dec {
         range = 0xFFFFFFFFu;
         for (int i = 0; i < 5; i++) code = (code << 8) | rd_byte();   // RangeDecoder.Init
         uint32_t state = 0, rep0 = 0, rep1 = 0, rep2 = 0, rep3 = 0;
+        uint32_t mb_next = 0;   // out[now - rep0 - 1] after a copy (the next literal's match byte)
         uint32_t now = 0;
         uint32_t prev = 0;
         int rc = LZMA_OK;
@@ -291,8 +298,8 @@ struct Dec {
             const uint32_t ps = now & ps_mask;
             // literal prefetch, issued before the isMatch decision: the coder's tree
             // (nodes 0-255) and, in matched mode, the 8 nodes along the match byte
-            const bool matched = !st_is_char(state);
-            const uint32_t mb = matched ? byte_back(now, rep0 + 1) : 0u;
+            const bool matched = !st_is_char(state);   // only right after a match / rep: copy() left mb
+            const uint32_t mb = matched ? mb_next : 0u;
             uint16_t* sub = lit + (size_t)(((now & ((1u << lp) - 1)) << lc) + (prev >> (8 - lc))) * 0x300;
             T256 tt;
             uint32_t mv[kVS];
@@ -393,7 +400,7 @@ struct Dec {
                     rc = LZMA_E_OVERFLOW;
                     break;
                 }
-                copy(now, d1, len);
+                mb_next = copy(now, d1, len);
                 now += len;
                 prev = win[(now - 1) & (kWin - 1)];
             }
