@@ -1169,6 +1169,7 @@ struct Enc {
                 }
             }
         }
+        __builtin_unreachable();   // the loop returns
     }
 
     // ------------------------------------------------------------ emitters (Encoder.java:860-1024, 818-841)

@@ -18,8 +18,6 @@
 // Output per position: minfo = count | main_len << 16 (main_len = longest
 // pair extended past fb as Encoder.ReadMatchDistances does, Encoder.java:
 // 275-287), kInlinePairs packed pairs inline, the rest in an overflow pool.
-#include <hipcub/hipcub.hpp>
-
 #include "lzma_common.h"
 #include "runtime.h"
 
@@ -133,39 +131,111 @@ __global__ void __launch_bounds__(64) mf_prev2_kernel(const uint64_t* __restrict
     }
 }
 
-// chain heads of the hash4 sort. The sorts are segmented per stream, so each
-// stream's non-inserted tail (sentinel keys) ends its own segment; a sentinel run
-// is a chain of its own that mf_chain_len_kernel empties.
-__global__ void __launch_bounds__(256) mf_heads_kernel(const uint64_t* __restrict__ keys, uint64_t total,
-                                                       uint8_t* __restrict__ flag, uint64_t* __restrict__ nvalid) {
-    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < total; i += (uint64_t)gridDim.x * blockDim.x) {
-        flag[i] = i == 0 || keys[i - 1] != keys[i];
-        if (i + 1 == total) *nvalid = total;
+// exclusive prefix sum of v over the block's threads; wsum: (blockDim / 64) words of LDS.
+// One block barrier; the caller synchronises before wsum is written again.
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* wsum) {
+    const uint32_t tid = threadIdx.x, lane = tid % 64, w = tid / 64;
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, (unsigned)o, 64);
+        if (lane >= (uint32_t)o) x += y;
     }
+    if (lane == 63) wsum[w] = x;
+    __syncthreads();
+    uint32_t before = 0;
+    for (uint32_t q = 0; q < w; q++) before += wsum[q];
+    return before + x - v;
 }
 
-// chain lengths, and the walk-order key (stream ascending, length descending,
-// lengths clamped at 1023: the order only shapes locality and lane balance):
-// the walk then works through the streams in order, so the lanes resident at
-// one time read a few streams' bytes (cache-resident) instead of the whole batch
-__global__ void __launch_bounds__(256) mf_chain_len_kernel(const uint32_t* __restrict__ starts, const uint64_t* __restrict__ nchains_p,
-                                                           const uint64_t* __restrict__ nvalid_p, const uint64_t* __restrict__ keys,
-                                                           uint32_t key_shift, uint32_t* __restrict__ lens,
-                                                           uint32_t* __restrict__ order_key) {
-    uint64_t nchains = *nchains_p, nvalid = *nvalid_p;
-    for (uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; c < nchains; c += (uint64_t)gridDim.x * blockDim.x) {
-        uint64_t e = (c + 1 < nchains) ? starts[c + 1] : nvalid;
-        const uint64_t k = keys[starts[c]];
-        if (k == kSentinel) {   // positions with no insertion: nothing to walk, ordered last
-            lens[c] = 0;
-            order_key[c] = ~0u;
-            continue;
-        }
-        const uint32_t len = (uint32_t)(e - starts[c]);
-        lens[c] = len;
-        const uint32_t stream = (uint32_t)(k >> key_shift);   // < 2^14 streams per pass
-        order_key[c] = (stream << 10) | (0x3FFu - (len < 0x3FFu ? len : 0x3FFu));   // 24 bits: 3 digit passes
+// Walk-order key of a chain: longest first (lanes of one wave walk similar-length
+// buckets); exact below 128, then 8 steps per doubling. Only the order depends on it.
+__device__ __forceinline__ uint32_t chain_order_key(uint32_t len) {
+    uint32_t f = len;
+    if (len >= 128) {
+        const uint32_t lg = 31u - (uint32_t)__clz((int)len);                 // >= 7
+        f = 128u + 8u * (lg - 7u) + ((len >> (lg - 3u)) & 7u);
+        if (f > 255u) f = 255u;
     }
+    return 255u - f;
+}
+
+// The chain (bucket) lists of one stream, one workgroup per stream: chain k of the
+// stream (its k-th bucket in sorted order) at index lo + k gets its first sorted index,
+// its length, its walk-order key and its own index (for the order sort);
+// seg_end[s] = lo + chains.
+// Sentinel keys (no insertion) sort last in their stream and form no chain.
+constexpr uint32_t kChainThreads = 256, kChainItems = 4;
+__global__ void __launch_bounds__(kChainThreads) mf_chains_kernel(const uint64_t* __restrict__ offs, const uint64_t* __restrict__ keys,
+                                                                   uint32_t* __restrict__ chain_start, uint32_t* __restrict__ chain_len,
+                                                                   uint32_t* __restrict__ okey, uint32_t* __restrict__ cidx,
+                                                                   uint64_t* __restrict__ seg_end) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];   // dynamic LDS (the CPU emulation shares it)
+    uint32_t* wsum = (uint32_t*)smem;                                   // [kChainThreads / 64]
+    uint32_t* tile_tot = wsum + kChainThreads / 64;                     // [2]: heads, valid items
+    const uint32_t tid = threadIdx.x, s = blockIdx.x;
+    const uint64_t lo = offs[s], n = offs[s + 1] - lo;
+    uint32_t run = 0, valid = 0;
+    for (uint64_t t0 = 0; t0 < n; t0 += kChainThreads * kChainItems) {
+        uint32_t head = 0, nv = 0;   // bit j: item j is a chain head
+        const uint64_t b0 = t0 + (uint64_t)tid * kChainItems;
+#pragma unroll
+        for (uint32_t j = 0; j < kChainItems; j++) {
+            const uint64_t i = b0 + j;
+            if (i < n) {
+                const uint64_t k = keys[lo + i];
+                const bool live = k != kSentinel;
+                nv += live;
+                if (live && (i == 0 || keys[lo + i - 1] != k)) head |= 1u << j;
+            }
+        }
+        const uint32_t cnt = (uint32_t)__builtin_popcount(head);
+        const uint32_t ex = block_excl_scan(cnt, wsum);
+        uint32_t c = run + ex;
+#pragma unroll
+        for (uint32_t j = 0; j < kChainItems; j++)
+            if (head & (1u << j)) chain_start[lo + c++] = (uint32_t)(lo + b0 + j);
+        if (tid == kChainThreads - 1) tile_tot[0] = ex + cnt;
+        const uint32_t vex = block_excl_scan(nv, wsum + 0);   // barrier inside: tile_tot[0] is visible after it
+        if (tid == kChainThreads - 1) tile_tot[1] = vex + nv;
+        __syncthreads();
+        run += tile_tot[0];
+        valid += tile_tot[1];
+        __syncthreads();
+    }
+    __syncthreads();
+    const uint32_t nch = run;
+    for (uint32_t c = tid; c < nch; c += kChainThreads) {
+        const uint32_t st = chain_start[lo + c];
+        const uint32_t en = c + 1 < nch ? chain_start[lo + c + 1] : (uint32_t)(lo + valid);
+        const uint32_t len = en - st;
+        chain_len[lo + c] = len;
+        okey[lo + c] = chain_order_key(len);
+        cidx[lo + c] = (uint32_t)(lo + c);
+    }
+    if (tid == 0) seg_end[s] = lo + nch;
+}
+
+// Exclusive scan of the streams' chain counts (one workgroup): chain_offs[s] = the
+// stream's first index in the compacted walk order, chain_offs[nstreams] = all chains.
+__global__ void __launch_bounds__(kChainThreads) mf_chain_scan_kernel(const uint64_t* __restrict__ offs, const uint64_t* __restrict__ seg_end,
+                                                                       int nstreams, uint64_t* __restrict__ chain_offs) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    uint32_t* wsum = (uint32_t*)smem;
+    uint32_t* tile_tot = wsum + kChainThreads / 64;
+    const uint32_t tid = threadIdx.x;
+    uint64_t run = 0;
+    for (int s0 = 0; s0 < nstreams; s0 += (int)kChainThreads) {
+        const int s = s0 + (int)tid;
+        const uint32_t v = s < nstreams ? (uint32_t)(seg_end[s] - offs[s]) : 0u;   // < 2^32 positions per pass
+        const uint32_t ex = block_excl_scan(v, wsum);
+        if (s < nstreams) chain_offs[s] = run + ex;
+        if (tid == kChainThreads - 1) tile_tot[0] = ex + v;
+        __syncthreads();
+        run += tile_tot[0];
+        __syncthreads();
+    }
+    if (tid == 0) chain_offs[nstreams] = run;
 }
 
 // Unaligned 8-byte little-endian load from a buffer padded by >= 16 bytes.
@@ -255,14 +325,13 @@ __global__ void __launch_bounds__(64) mf_walk_kernel(const uint8_t* __restrict__
                                                      const uint32_t* __restrict__ chain_order,
                                                      const uint32_t* __restrict__ chain_start,
                                                      const uint32_t* __restrict__ chain_len,
-                                                     const uint64_t* __restrict__ nchains_p,
+                                                     uint64_t nchains,
                                                      MfArgs a, WNode* __restrict__ nodes, PairT* __restrict__ pairs,
                                                      uint32_t* __restrict__ ovf_off, PairT* __restrict__ ovf,
                                                      unsigned long long* __restrict__ ovf_used, uint64_t ovf_cap,
                                                      uint32_t ovf_stride,
                                                      int* __restrict__ err) {
     using PP = PairPack<PairT>;
-    uint64_t nchains = *nchains_p;
     // XCD-aware mapping: the dispatcher places block b on XCD b % 8, so XCD x takes
     // the x-th eighth of the (stream-ordered) chain list and its L2 serves a few streams
     const uint32_t per_xcd = gridDim.x / 8;   // the host pads the grid to a multiple of 8
@@ -417,43 +486,6 @@ __global__ void __launch_bounds__(64) mf_walk_kernel(const uint8_t* __restrict__
 
 static inline uint32_t bits_for(uint64_t v) { uint32_t b = 0; while (b < 64 && (v >> b) != 0) b++; return b; }
 
-template <typename KeyT, typename ValT>
-static int radix_sort(Ctx* ctx, const KeyT* kin, KeyT* kout, const ValT* vin, ValT* vout, uint64_t n, int end_bit,
-                      hipStream_t st, bool descending = false) {
-    size_t tmp = 0;
-    hipError_t e;
-    if (descending)
-        e = hipcub::DeviceRadixSort::SortPairsDescending(nullptr, tmp, kin, kout, vin, vout, (int)n, 0, end_bit, st);
-    else
-        e = hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, kin, kout, vin, vout, (int)n, 0, end_bit, st);
-    if (e != hipSuccess) return ctx->fail(LZMA_E_DEVICE, "radix sort sizing: %s", hipGetErrorString(e));
-    void* t = ctx->scratch(tmp);
-    if (!t && tmp) return ctx->fail(LZMA_E_NOMEM, "radix sort temp %zu", tmp);
-    if (descending)
-        e = hipcub::DeviceRadixSort::SortPairsDescending(t, tmp, kin, kout, vin, vout, (int)n, 0, end_bit, st);
-    else
-        e = hipcub::DeviceRadixSort::SortPairs(t, tmp, kin, kout, vin, vout, (int)n, 0, end_bit, st);
-    if (e != hipSuccess) return ctx->fail(LZMA_E_DEVICE, "radix sort: %s", hipGetErrorString(e));
-    return LZMA_OK;
-}
-
-// Stable sort of each stream's positions by the low `end_bit` key bits: the
-// positions are stream-major already, so the stream bits need no digit passes.
-template <typename KeyT, typename ValT>
-static int segmented_sort(Ctx* ctx, const KeyT* kin, KeyT* kout, const ValT* vin, ValT* vout, uint64_t n,
-                          const uint64_t* d_offs, int nstreams, int end_bit, hipStream_t st) {
-    size_t tmp = 0;
-    hipError_t e = hipcub::DeviceSegmentedRadixSort::SortPairs(nullptr, tmp, kin, kout, vin, vout, (int)n, nstreams, d_offs,
-                                                              d_offs + 1, 0, end_bit, st);
-    if (e != hipSuccess) return ctx->fail(LZMA_E_DEVICE, "segmented sort sizing: %s", hipGetErrorString(e));
-    void* t = ctx->scratch(tmp);
-    if (!t && tmp) return ctx->fail(LZMA_E_NOMEM, "segmented sort temp %zu", tmp);
-    e = hipcub::DeviceSegmentedRadixSort::SortPairs(t, tmp, kin, kout, vin, vout, (int)n, nstreams, d_offs, d_offs + 1, 0,
-                                                   end_bit, st);
-    if (e != hipSuccess) return ctx->fail(LZMA_E_DEVICE, "segmented sort: %s", hipGetErrorString(e));
-    return LZMA_OK;
-}
-
 static inline unsigned grid_for(uint64_t n, unsigned block, unsigned cap = 65536) {
     uint64_t g = (n + block - 1) / block;
     if (g < 1) g = 1;
@@ -497,34 +529,26 @@ int run_match_finder(Ctx* ctx, const Derived& d, const uint8_t* in, const uint64
         if ((rc = seg_radix_sort(ctx, true, w.k4, w.vals, w.ks, w.vs, w.son, w.son + total, w.hist, total, d_offs, nstreams,
                                  (int)(bt4 ? d.hash_bits : 16), st))) return rc;
     }
-    hipMemsetAsync(w.counts, 0, 2 * sizeof(uint64_t), st);   // [0]=nvalid [1]=nchains
-    hipLaunchKernelGGL(mf_heads_kernel, dim3(grid_for(total, B)), dim3(B), 0, st, w.ks, total, w.flag, w.counts);
-    {
-        size_t tmp = 0;
-        hipcub::CountingInputIterator<uint32_t> it(0);
-        hipcub::DeviceSelect::Flagged(nullptr, tmp, it, w.flag, w.chain_start, w.counts + 1, (int)total, st);
-        void* t = ctx->scratch(tmp);
-        if (!t && tmp) return ctx->fail(LZMA_E_NOMEM, "select temp");
-        hipcub::DeviceSelect::Flagged(t, tmp, it, w.flag, w.chain_start, w.counts + 1, (int)total, st);
-    }
-    LZG_TRACE(ctx, st, "mf sorts + chain select done");
-    uint64_t hc[2];
-    hipMemcpyAsync(hc, w.counts, sizeof(hc), hipMemcpyDeviceToHost, st);
-    if (hipStreamSynchronize(st) != hipSuccess) return ctx->fail(LZMA_E_DEVICE, "sync after chain select");
-    uint64_t nchains = hc[1];
-    if (nchains == 0) return LZMA_OK;
-    // walk order: stream by stream (cache locality), longest chains first within a
-    // stream (lanes of one wave walk similar-length buckets). The k2/k3 key arrays are
-    // dead here and hold the order keys.
+    // chain lists and walk order: stream by stream (cache locality), longest chains first
+    // within a stream (lanes of one wave walk similar-length buckets). The k2/k3 key
+    // arrays are dead here and hold the order keys.
     uint32_t* okey = (uint32_t*)w.k2;
     uint32_t* okey_sorted = (uint32_t*)w.k3;
-    hipLaunchKernelGGL(mf_chain_len_kernel, dim3(grid_for(nchains, B)), dim3(B), 0, st, w.chain_start, w.counts + 1, w.counts,
-                       w.ks, bt4 ? d.hash_bits : 16u, w.chain_len, okey);
     {
         TimedLaunch tl(ctx, "mf_sort", st);
-        hipLaunchKernelGGL(iota_kernel, dim3(grid_for(nchains, B)), dim3(B), 0, st, w.chain_idx, nchains);
-        if ((rc = radix_sort(ctx, okey, okey_sorted, w.chain_idx, w.chain_order, nchains, 24, st))) return rc;
+        hipLaunchKernelGGL(mf_chains_kernel, dim3(nstreams), dim3(kChainThreads), (kChainThreads / 64 + 2) * 4, st, d_offs, w.ks,
+                           w.chain_start, w.chain_len, okey, w.chain_idx, w.seg_end);
+        hipLaunchKernelGGL(mf_chain_scan_kernel, dim3(1), dim3(kChainThreads), (kChainThreads / 64 + 2) * 4, st, d_offs, w.seg_end,
+                           nstreams, w.chain_offs);
+        if ((rc = seg_radix_sort(ctx, false, okey, w.chain_idx, okey_sorted, w.chain_order, w.son, w.son + total, w.hist, total,
+                                 d_offs, nstreams, 8, st, w.seg_end, w.chain_offs))) return rc;
     }
+    uint64_t nchains = 0;   // sizes the walk grid: one host round trip per pass
+    if (hipMemcpyAsync(&nchains, w.chain_offs + nstreams, sizeof(nchains), hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+        return ctx->fail(LZMA_E_DEVICE, "mf: chain count: %s", hipGetErrorString(hipGetLastError()));
+    LZG_TRACE(ctx, st, "mf sorts + chain lists done");
+    if (nchains == 0) return LZMA_OK;
     hipMemsetAsync(w.ovf_used, 0, sizeof(unsigned long long), st);
     hipMemsetAsync(w.err, 0, sizeof(int), st);
     {
@@ -535,11 +559,11 @@ int run_match_finder(Ctx* ctx, const Derived& d, const uint8_t* in, const uint64
         // experiment: dynamic LDS per wave caps the waves per CU (L2 working set)
         static const size_t walk_lds = getenv("LZG_WALK_LDS") ? (size_t)atoi(getenv("LZG_WALK_LDS")) : 0;
         if (wide_pairs) {
-            if (bt4) hipLaunchKernelGGL((mf_walk_kernel<uint64_t, true>), dim3(grid), dim3(WB), walk_lds, st, in, d_offs, w.ks, w.vs, w.chain_order, w.chain_start, w.chain_len, w.counts + 1, a, (WNode*)w.son, (uint64_t*)w.pairs, w.ovf_off, (uint64_t*)w.ovf, w.ovf_used, w.ovf_cap, ovf_stride(d.fb), w.err);
-            else hipLaunchKernelGGL((mf_walk_kernel<uint64_t, false>), dim3(grid), dim3(WB), walk_lds, st, in, d_offs, w.ks, w.vs, w.chain_order, w.chain_start, w.chain_len, w.counts + 1, a, (WNode*)w.son, (uint64_t*)w.pairs, w.ovf_off, (uint64_t*)w.ovf, w.ovf_used, w.ovf_cap, ovf_stride(d.fb), w.err);
+            if (bt4) hipLaunchKernelGGL((mf_walk_kernel<uint64_t, true>), dim3(grid), dim3(WB), walk_lds, st, in, d_offs, w.ks, w.vs, w.chain_order, w.chain_start, w.chain_len, nchains, a, (WNode*)w.son, (uint64_t*)w.pairs, w.ovf_off, (uint64_t*)w.ovf, w.ovf_used, w.ovf_cap, ovf_stride(d.fb), w.err);
+            else hipLaunchKernelGGL((mf_walk_kernel<uint64_t, false>), dim3(grid), dim3(WB), walk_lds, st, in, d_offs, w.ks, w.vs, w.chain_order, w.chain_start, w.chain_len, nchains, a, (WNode*)w.son, (uint64_t*)w.pairs, w.ovf_off, (uint64_t*)w.ovf, w.ovf_used, w.ovf_cap, ovf_stride(d.fb), w.err);
         } else {
-            if (bt4) hipLaunchKernelGGL((mf_walk_kernel<uint32_t, true>), dim3(grid), dim3(WB), walk_lds, st, in, d_offs, w.ks, w.vs, w.chain_order, w.chain_start, w.chain_len, w.counts + 1, a, (WNode*)w.son, (uint32_t*)w.pairs, w.ovf_off, (uint32_t*)w.ovf, w.ovf_used, w.ovf_cap, ovf_stride(d.fb), w.err);
-            else hipLaunchKernelGGL((mf_walk_kernel<uint32_t, false>), dim3(grid), dim3(WB), walk_lds, st, in, d_offs, w.ks, w.vs, w.chain_order, w.chain_start, w.chain_len, w.counts + 1, a, (WNode*)w.son, (uint32_t*)w.pairs, w.ovf_off, (uint32_t*)w.ovf, w.ovf_used, w.ovf_cap, ovf_stride(d.fb), w.err);
+            if (bt4) hipLaunchKernelGGL((mf_walk_kernel<uint32_t, true>), dim3(grid), dim3(WB), walk_lds, st, in, d_offs, w.ks, w.vs, w.chain_order, w.chain_start, w.chain_len, nchains, a, (WNode*)w.son, (uint32_t*)w.pairs, w.ovf_off, (uint32_t*)w.ovf, w.ovf_used, w.ovf_cap, ovf_stride(d.fb), w.err);
+            else hipLaunchKernelGGL((mf_walk_kernel<uint32_t, false>), dim3(grid), dim3(WB), walk_lds, st, in, d_offs, w.ks, w.vs, w.chain_order, w.chain_start, w.chain_len, nchains, a, (WNode*)w.son, (uint32_t*)w.pairs, w.ovf_off, (uint32_t*)w.ovf, w.ovf_used, w.ovf_cap, ovf_stride(d.fb), w.err);
         }
     }
     LZG_TRACE(ctx, st, "mf_walk done (%llu chains)", (unsigned long long)nchains);

@@ -156,7 +156,7 @@ __global__ void __launch_bounds__(kRcLanes) rc_range_kernel(RcArgs a) {
         const uint32_t bm = 0u - ((rec >> 11) & 1u);
         const int32_t q = (int32_t)((p ^ bm) - bm);
         const uint32_t t = range >> 11;
-        const uint32_t r1p = (range & bm) + (uint32_t)((int32_t)t * q);
+        const uint32_t r1p = (range & bm) + (uint32_t)((int64_t)(int32_t)t * q);   // |t*q| < 2^32: 24-bit operands, low word kept
         const uint32_t dm = 0u - (uint32_t)(p == 0);   // a direct bit: range >> 1 (a mask, not a branch)
         const uint32_t r1 = r1p ^ ((r1p ^ (range >> 1)) & dm);
         range = r1 << ((uint32_t)__builtin_clz(r1) & 8u);

@@ -38,6 +38,8 @@ struct MfBuffers {
     uint64_t* son;                // walk tree nodes (mf.hip WNode, 32 B per position: links + 16-byte prefix);
                                   // before the walk, the sorts' ping-pong buffers
     uint32_t* hist;               // sort.hip digit histograms, [nstreams][4][256]
+    uint64_t* seg_end;            // per stream: the end of its chain list (mf_chains_kernel)
+    uint64_t* chain_offs;         // per stream: where its chains start in the compacted walk order; [nstreams] = chains
     void* pairs;
     uint32_t* ovf_off;
     void* ovf;
@@ -218,7 +220,7 @@ int run_match_finder(Ctx* ctx, const Derived& d, const uint8_t* in, const uint64
 // sort.hip: stable per-stream radix sort by the low end_bit key bits
 int seg_radix_sort(Ctx* ctx, bool key64, const void* kin, const uint32_t* vin, void* kout, uint32_t* vout,
                    uint64_t* tmp_a, uint64_t* tmp_b, uint32_t* hist, uint64_t n, const uint64_t* d_offs, int nstreams,
-                   int end_bit, hipStream_t st);
+                   int end_bit, hipStream_t st, const uint64_t* d_ends = nullptr, const uint64_t* d_dofs = nullptr);
 
 struct EncArgs {
     const uint8_t* in;            // padded batch copy

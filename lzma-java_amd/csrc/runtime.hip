@@ -142,6 +142,8 @@ static int encode_pass(Ctx* ctx, const Derived& d, const uint8_t* d_in, const ui
             w.counts = c.take<uint64_t>(2);
             w.son = c.take<uint64_t>(4 * T);   // mf.hip WNode: 32 bytes per position
             w.hist = c.take<uint32_t>((size_t)ns * 1024);
+            w.seg_end = c.take<uint64_t>((size_t)ns + 1);
+            w.chain_offs = c.take<uint64_t>((size_t)ns + 1);
         };
         size_t p1_bytes;
         {

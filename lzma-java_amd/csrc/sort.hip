@@ -43,6 +43,8 @@ struct SortPass {
     void* kout;               // packed items, or the final keys
     uint32_t* vout;           // final positions (last pass only)
     const uint64_t* offs;     // stream offsets (nstreams + 1), relative to the pass
+    const uint64_t* ends;     // segment ends (segment s = [offs[s], ends[s])), or null: offs[s + 1]
+    const uint64_t* dofs;     // where the last pass writes segment s (compaction), or null: offs[s]
     const uint32_t* hist;     // [nstreams][kMaxPasses][256]
     uint32_t pass, shift, bits, end_bit;
 };
@@ -79,7 +81,7 @@ __global__ void __launch_bounds__(kSortThreads) seg_hist_kernel(SortPass a, uint
     for (uint32_t k = tid; k < kSortWaves * kMaxPasses * 256; k += kSortThreads) (&h[0][0][0])[k] = 0;
     __syncthreads();
     const uint32_t s = blockIdx.x;
-    const uint64_t lo = a.offs[s], n = a.offs[s + 1] - lo;
+    const uint64_t lo = a.offs[s], n = (a.ends ? a.ends[s] : a.offs[s + 1]) - lo;
     for (uint64_t i = tid; i < n; i += kSortThreads) {
         const uint64_t it = load_item<IN>(a, lo + i, a.end_bit);
         const uint32_t hb = (uint32_t)(it >> 32) & 0x7FFFFFFFu;
@@ -109,7 +111,7 @@ __global__ void __launch_bounds__(kSortThreads) seg_pass_kernel(SortPass a) {
     auto cnt = (uint32_t(*)[256])(scan + 256);                           // [kSortWaves][256]
     const uint32_t tid = threadIdx.x, w = tid / kSW, lane = tid % kSW;
     const uint32_t s = blockIdx.x;
-    const uint64_t lo = a.offs[s], n = a.offs[s + 1] - lo;
+    const uint64_t lo = a.offs[s], n = (a.ends ? a.ends[s] : a.offs[s + 1]) - lo;
     const uint32_t nb = 1u << a.bits, dmask = nb - 1;
     // bucket bases of this stream: exclusive scan of its histogram (Hillis-Steele in LDS)
     const uint32_t hv = tid < nb ? a.hist[((size_t)s * kMaxPasses + a.pass) * 256 + tid] : 0u;
@@ -179,7 +181,7 @@ __global__ void __launch_bounds__(kSortThreads) seg_pass_kernel(SortPass a) {
         for (uint32_t j = tid; j < tn; j += kSortThreads) {
             const uint64_t it = tile[j];
             const uint32_t d = (uint32_t)(it >> (32 + a.shift)) & dmask;
-            const uint64_t dst = lo + base[d] + (j - loff[d]);
+            const uint64_t dst = (OUT != SK_PACKED && a.dofs ? a.dofs[s] : lo) + base[d] + (j - loff[d]);
             if (OUT == SK_PACKED) {
                 ((uint64_t*)a.kout)[dst] = it;
             } else {
@@ -205,9 +207,11 @@ static void launch_pass(const SortPass& p, int nstreams, hipStream_t st) {
 
 // Stable sort of every stream's items by the low end_bit bits of their keys.
 // key64: keys are u64 (else u32); tmp_a / tmp_b: n u64 each; hist: nstreams * 1024 u32.
+// d_ends (optional): segment s is [offs[s], ends[s]); d_dofs (optional): the sorted
+// segment s is written from d_dofs[s] on (the segments compacted into one list).
 int seg_radix_sort(Ctx* ctx, bool key64, const void* kin, const uint32_t* vin, void* kout, uint32_t* vout,
                    uint64_t* tmp_a, uint64_t* tmp_b, uint32_t* hist, uint64_t n, const uint64_t* d_offs, int nstreams,
-                   int end_bit, hipStream_t st) {
+                   int end_bit, hipStream_t st, const uint64_t* d_ends, const uint64_t* d_dofs) {
     if (n == 0 || nstreams <= 0) return LZMA_OK;
     if (end_bit < 1 || end_bit > 31) return ctx->fail(LZMA_E_INTERNAL, "seg_radix_sort: %d key bits", end_bit);
     const uint32_t npass = (uint32_t)(end_bit + 7) / 8;
@@ -220,7 +224,7 @@ int seg_radix_sort(Ctx* ctx, bool key64, const void* kin, const uint32_t* vin, v
         if (width[q] > 8) return ctx->fail(LZMA_E_INTERNAL, "seg_radix_sort: %u-bit digit", width[q]);   // LDS tables hold 256
     }
     SortPass p{};
-    p.kin = kin; p.vin = vin; p.offs = d_offs; p.hist = hist; p.end_bit = (uint32_t)end_bit;
+    p.kin = kin; p.vin = vin; p.offs = d_offs; p.ends = d_ends; p.dofs = d_dofs; p.hist = hist; p.end_bit = (uint32_t)end_bit;
     if (key64) hipLaunchKernelGGL((seg_hist_kernel<SK_KEY64>), dim3(nstreams), dim3(kSortThreads), kHistLds, st, p, npass, widths, hist);
     else hipLaunchKernelGGL((seg_hist_kernel<SK_KEY32>), dim3(nstreams), dim3(kSortThreads), kHistLds, st, p, npass, widths, hist);
     uint32_t shift = 0;
