@@ -166,8 +166,7 @@ struct Enc {
     uint16_t* recs;           // the stream's coder records in HBM (rc.hip codes them)
     uint64_t rcap, rpos;      // record capacity / records emitted
     uint32_t overflow;
-    const uint32_t* minfo;
-    const PairT* pairs;
+    const v4u32* pairs;        // per-position match-list records
     const uint32_t* ovf_off;
     const PairT* ovf;
     uint64_t gbase;
@@ -599,10 +598,9 @@ struct Enc {
             if (q < n) {
                 uint64_t g0 = gbase + q;
                 // streamed once: non-temporal, so they do not evict the literal models from L2
-                info = __builtin_nontemporal_load(minfo + g0);
-                const PairT* src = pairs + g0 * kInlinePairs;
-                p0 = __builtin_nontemporal_load(src + 0); p1 = __builtin_nontemporal_load(src + 1);
-                p2 = __builtin_nontemporal_load(src + 2); p3 = __builtin_nontemporal_load(src + 3);
+                PairT q[kInlinePairs];
+                info = load_rec<PairT>(pairs + g0 * rec_vecs<PairT>(), q);
+                p0 = q[0]; p1 = q[1]; p2 = q[2]; p3 = q[3];
             }
             ring_info[k] = info;
             PairT* dst = ring_pairs + k * kInlinePairs;
@@ -1391,8 +1389,7 @@ __global__ void __launch_bounds__(kWave, 4) enc_kernel(EncArgs a) {
 #ifdef LZG_DEBUG
     if (e.dbg && blockIdx.x == 0 && e.lane == 0) __hip_atomic_store(e.dbg, 7u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 #endif
-    e.minfo = a.minfo;
-    e.pairs = (const PairT*)a.pairs;
+    e.pairs = a.pairs;
     e.ovf_off = a.ovf_off;
     e.ovf = (const PairT*)a.ovf;
     // One workgroup per stream, longest first (order[]): the dispatcher is the

@@ -252,4 +252,43 @@ template <> struct PairPack<uint64_t> {
 };
 constexpr int kInlinePairs = 4;
 
+// Per-position match-list record (mf_walk writes it, the parser reads it): the
+// first kInlinePairs pairs, then the info word (pair count | extended longest
+// length << 16) in a vector of its own. One lane writes a whole record with
+// 16-byte stores, so every 32-byte sector it touches is written in full (the
+// u32 record is exactly one sector) -- no partial-sector write-back from L2.
+typedef uint32_t v4u32 __attribute__((vector_size(16)));
+template <typename PairT> constexpr uint32_t rec_vecs() { return (uint32_t)(sizeof(PairT) * kInlinePairs / 16 + 1); }
+inline uint32_t rec_bytes(bool wide) { return 16u * (wide ? rec_vecs<uint64_t>() : rec_vecs<uint32_t>()); }
+
+template <typename PairT>
+__device__ inline void store_rec(v4u32* r, PairT q0, PairT q1, PairT q2, PairT q3, uint32_t info) {
+    const v4u32 iv = {info, 0u, 0u, 0u};
+    if constexpr (sizeof(PairT) == 4) {
+        const v4u32 pv = {q0, q1, q2, q3};
+        __builtin_nontemporal_store(pv, r + 0);
+        __builtin_nontemporal_store(iv, r + 1);
+    } else {
+        const v4u32 pa = {(uint32_t)q0, (uint32_t)(q0 >> 32), (uint32_t)q1, (uint32_t)(q1 >> 32)};
+        const v4u32 pb = {(uint32_t)q2, (uint32_t)(q2 >> 32), (uint32_t)q3, (uint32_t)(q3 >> 32)};
+        __builtin_nontemporal_store(pa, r + 0);
+        __builtin_nontemporal_store(pb, r + 1);
+        __builtin_nontemporal_store(iv, r + 2);
+    }
+}
+
+template <typename PairT>
+__device__ inline uint32_t load_rec(const v4u32* r, PairT* q) {
+    if constexpr (sizeof(PairT) == 4) {
+        const v4u32 pv = __builtin_nontemporal_load(r + 0);
+        q[0] = pv[0]; q[1] = pv[1]; q[2] = pv[2]; q[3] = pv[3];
+        return __builtin_nontemporal_load(r + 1)[0];
+    } else {
+        const v4u32 pa = __builtin_nontemporal_load(r + 0), pb = __builtin_nontemporal_load(r + 1);
+        q[0] = pa[0] | ((uint64_t)pa[1] << 32); q[1] = pa[2] | ((uint64_t)pa[3] << 32);
+        q[2] = pb[0] | ((uint64_t)pb[1] << 32); q[3] = pb[2] | ((uint64_t)pb[3] << 32);
+        return __builtin_nontemporal_load(r + 2)[0];
+    }
+}
+
 }  // namespace lzg

@@ -15,9 +15,10 @@
 //                  (:152-273) for the bucket's positions in order, with the
 //                  son[] links indexed by sorted bucket index (window expiry
 //                  via matchMinPos makes cyclic reuse unobservable).
-// Output per position: minfo = count | main_len << 16 (main_len = longest
-// pair extended past fb as Encoder.ReadMatchDistances does, Encoder.java:
-// 275-287), kInlinePairs packed pairs inline, the rest in an overflow pool.
+// Output per position: a record (lzma_common.h store_rec) of kInlinePairs
+// packed pairs and info = count | main_len << 16 (main_len = longest pair
+// extended past fb as Encoder.ReadMatchDistances does, Encoder.java:275-287);
+// the pairs past kInlinePairs go to an overflow pool.
 #include "lzma_common.h"
 #include "runtime.h"
 
@@ -49,13 +50,15 @@ __global__ void __launch_bounds__(256) mf_keys_kernel(const uint8_t* __restrict_
     while (s + 1 < nstreams && offs[s + 1] <= g) s++;
     if (g < total) {
         uint64_t base = offs[s], n = offs[s + 1] - base, p = g - base;
-        a.minfo[g] = 0;
         a.vals[g] = (uint32_t)g;
         uint64_t rem = n - p;
         uint32_t len_limit = rem < a.fb ? (uint32_t)rem : a.fb;
         if (len_limit < a.min_match_check) {   // BinTree.java:153-162: no insertion
             a.k4[g] = kSentinel;
             if (BT4) { a.k3[g] = kSentinel32; a.k2[g] = kSentinel32; }
+            // the walk skips this position: its record says "no pairs" (every other
+            // position's record is written by the walk)
+            a.mrec[g * a.rec_vecs + a.rec_vecs - 1] = v4u32{0u, 0u, 0u, 0u};
             return;
         }
         uint32_t b0 = in[g], b1 = in[g + 1];
@@ -326,7 +329,7 @@ __global__ void __launch_bounds__(64) mf_walk_kernel(const uint8_t* __restrict__
                                                      const uint32_t* __restrict__ chain_start,
                                                      const uint32_t* __restrict__ chain_len,
                                                      uint64_t nchains,
-                                                     MfArgs a, WNode* __restrict__ nodes, PairT* __restrict__ pairs,
+                                                     MfArgs a, WNode* __restrict__ nodes, v4u32* __restrict__ recs,
                                                      uint32_t* __restrict__ ovf_off, PairT* __restrict__ ovf,
                                                      unsigned long long* __restrict__ ovf_used, uint64_t ovf_cap,
                                                      uint32_t ovf_stride,
@@ -471,12 +474,7 @@ __global__ void __launch_bounds__(64) mf_walk_kernel(const uint8_t* __restrict__
         nodes[i] = self;
         head = self;
         // outputs are touched once: non-temporal, so the stream's nodes and bytes keep the L2
-        PairT* inl = pairs + g * kInlinePairs;
-        __builtin_nontemporal_store(q0, inl + 0);
-        __builtin_nontemporal_store(q1, inl + 1);
-        __builtin_nontemporal_store(q2, inl + 2);
-        __builtin_nontemporal_store(q3, inl + 3);
-        __builtin_nontemporal_store(cnt | (ml << 16), a.minfo + g);
+        store_rec<PairT>(recs + g * rec_vecs<PairT>(), q0, q1, q2, q3, cnt | (ml << 16));
         prev_local = pos;
         g = g_next;
     }
@@ -493,7 +491,7 @@ static inline unsigned grid_for(uint64_t n, unsigned block, unsigned cap = 65536
 }
 
 // Runs K1..K4 for one batch. in: padded device copy of the batch; offs: device
-// stream offsets (nstreams+1). Fills w.minfo / w.pairs / w.ovf_off / w.ovf.
+// stream offsets (nstreams+1). Fills w.pairs (records) / w.ovf_off / w.ovf.
 int run_match_finder(Ctx* ctx, const Derived& d, const uint8_t* in, const uint64_t* d_offs, int nstreams,
                      uint64_t total, bool wide_pairs, MfBuffers& w, hipStream_t st) {
     if (total == 0) return LZMA_OK;
@@ -501,7 +499,7 @@ int run_match_finder(Ctx* ctx, const Derived& d, const uint8_t* in, const uint64
     MfArgs a{};
     a.fb = d.fb; a.min_match_check = d.min_match_check; a.hash_mask = d.hash_mask; a.hash_bits = d.hash_bits;
     a.cut_value = d.cut_value; a.cyc_size = d.cyc_size; a.direct_bytes = d.direct_bytes;
-    a.k4 = w.k4; a.k3 = (uint32_t*)w.k3; a.k2 = (uint32_t*)w.k2; a.vals = w.vals; a.minfo = w.minfo; a.prev2 = w.prev2; a.prev3 = w.prev3;
+    a.k4 = w.k4; a.k3 = (uint32_t*)w.k3; a.k2 = (uint32_t*)w.k2; a.vals = w.vals; a.mrec = w.pairs; a.rec_vecs = wide_pairs ? rec_vecs<uint64_t>() : rec_vecs<uint32_t>(); a.prev2 = w.prev2; a.prev3 = w.prev3;
     const bool bt4 = d.hash_array != 0;
     const unsigned B = 256;
     {
@@ -559,11 +557,11 @@ int run_match_finder(Ctx* ctx, const Derived& d, const uint8_t* in, const uint64
         // experiment: dynamic LDS per wave caps the waves per CU (L2 working set)
         static const size_t walk_lds = getenv("LZG_WALK_LDS") ? (size_t)atoi(getenv("LZG_WALK_LDS")) : 0;
         if (wide_pairs) {
-            if (bt4) hipLaunchKernelGGL((mf_walk_kernel<uint64_t, true>), dim3(grid), dim3(WB), walk_lds, st, in, d_offs, w.ks, w.vs, w.chain_order, w.chain_start, w.chain_len, nchains, a, (WNode*)w.son, (uint64_t*)w.pairs, w.ovf_off, (uint64_t*)w.ovf, w.ovf_used, w.ovf_cap, ovf_stride(d.fb), w.err);
-            else hipLaunchKernelGGL((mf_walk_kernel<uint64_t, false>), dim3(grid), dim3(WB), walk_lds, st, in, d_offs, w.ks, w.vs, w.chain_order, w.chain_start, w.chain_len, nchains, a, (WNode*)w.son, (uint64_t*)w.pairs, w.ovf_off, (uint64_t*)w.ovf, w.ovf_used, w.ovf_cap, ovf_stride(d.fb), w.err);
+            if (bt4) hipLaunchKernelGGL((mf_walk_kernel<uint64_t, true>), dim3(grid), dim3(WB), walk_lds, st, in, d_offs, w.ks, w.vs, w.chain_order, w.chain_start, w.chain_len, nchains, a, (WNode*)w.son, w.pairs, w.ovf_off, (uint64_t*)w.ovf, w.ovf_used, w.ovf_cap, ovf_stride(d.fb), w.err);
+            else hipLaunchKernelGGL((mf_walk_kernel<uint64_t, false>), dim3(grid), dim3(WB), walk_lds, st, in, d_offs, w.ks, w.vs, w.chain_order, w.chain_start, w.chain_len, nchains, a, (WNode*)w.son, w.pairs, w.ovf_off, (uint64_t*)w.ovf, w.ovf_used, w.ovf_cap, ovf_stride(d.fb), w.err);
         } else {
-            if (bt4) hipLaunchKernelGGL((mf_walk_kernel<uint32_t, true>), dim3(grid), dim3(WB), walk_lds, st, in, d_offs, w.ks, w.vs, w.chain_order, w.chain_start, w.chain_len, nchains, a, (WNode*)w.son, (uint32_t*)w.pairs, w.ovf_off, (uint32_t*)w.ovf, w.ovf_used, w.ovf_cap, ovf_stride(d.fb), w.err);
-            else hipLaunchKernelGGL((mf_walk_kernel<uint32_t, false>), dim3(grid), dim3(WB), walk_lds, st, in, d_offs, w.ks, w.vs, w.chain_order, w.chain_start, w.chain_len, nchains, a, (WNode*)w.son, (uint32_t*)w.pairs, w.ovf_off, (uint32_t*)w.ovf, w.ovf_used, w.ovf_cap, ovf_stride(d.fb), w.err);
+            if (bt4) hipLaunchKernelGGL((mf_walk_kernel<uint32_t, true>), dim3(grid), dim3(WB), walk_lds, st, in, d_offs, w.ks, w.vs, w.chain_order, w.chain_start, w.chain_len, nchains, a, (WNode*)w.son, w.pairs, w.ovf_off, (uint32_t*)w.ovf, w.ovf_used, w.ovf_cap, ovf_stride(d.fb), w.err);
+            else hipLaunchKernelGGL((mf_walk_kernel<uint32_t, false>), dim3(grid), dim3(WB), walk_lds, st, in, d_offs, w.ks, w.vs, w.chain_order, w.chain_start, w.chain_len, nchains, a, (WNode*)w.son, w.pairs, w.ovf_off, (uint32_t*)w.ovf, w.ovf_used, w.ovf_cap, ovf_stride(d.fb), w.err);
         }
     }
     LZG_TRACE(ctx, st, "mf_walk done (%llu chains)", (unsigned long long)nchains);

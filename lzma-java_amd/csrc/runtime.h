@@ -23,15 +23,17 @@ namespace lzg {
 
 struct MfArgs {
     uint32_t fb, min_match_check, hash_mask, hash_bits, cut_value, direct_bytes;
+    uint32_t rec_vecs;            // 16-byte vectors per match-list record
     uint64_t cyc_size;
     uint64_t* k4;
     uint32_t *k3, *k2;            // (stream << 16 | hash3), (stream << 10 | hash2): < 2^30 for <= 16384 streams
-    uint32_t *vals, *minfo, *prev2, *prev3;
+    uint32_t *vals, *prev2, *prev3;
+    v4u32* mrec;                  // per-position match-list records (lzma_common.h store_rec)
 };
 
 struct MfBuffers {
     uint64_t *k4, *k3, *k2, *ks;
-    uint32_t *vals, *vs, *minfo, *prev2, *prev3;
+    uint32_t *vals, *vs, *prev2, *prev3;
     uint8_t* flag;
     uint32_t *chain_start, *chain_len, *chain_len_sorted, *chain_idx, *chain_order;
     uint64_t* counts;
@@ -40,7 +42,7 @@ struct MfBuffers {
     uint32_t* hist;               // sort.hip digit histograms, [nstreams][4][256]
     uint64_t* seg_end;            // per stream: the end of its chain list (mf_chains_kernel)
     uint64_t* chain_offs;         // per stream: where its chains start in the compacted walk order; [nstreams] = chains
-    void* pairs;
+    v4u32* pairs;                 // per-position match-list records: inline pairs + info (lzma_common.h)
     uint32_t* ovf_off;
     void* ovf;
     uint64_t ovf_cap;
@@ -228,8 +230,7 @@ struct EncArgs {
     const uint32_t* order;        // processing order (longest first)
     int nstreams;
     unsigned int* next;           // work-queue counter
-    const uint32_t* minfo;
-    const void* pairs;
+    const v4u32* pairs;           // per-position match-list records (lzma_common.h store_rec)
     const uint32_t* ovf_off;
     const void* ovf;
     uint16_t* recs;               // coder records (rc.hip), per stream at rec_offs[s]

@@ -88,8 +88,8 @@ constexpr int kMaxStreamsPerPass = 16384;
 // Host copies of the match finder's per-position output (the instrumented
 // mode of SURVEY 7.1: lzma_match_lists diffs them against the oracle).
 struct MatchDump {
-    std::vector<uint32_t> minfo, ovf_off;
-    std::vector<uint8_t> pairs, ovf;
+    std::vector<uint32_t> ovf_off;
+    std::vector<uint8_t> recs, ovf;
     bool wide = false;
     uint32_t stride = 0;
 };
@@ -172,8 +172,7 @@ static int encode_pass(Ctx* ctx, const Derived& d, const uint8_t* d_in, const ui
             d_recs = (uint16_t*)u;
             Carver c1(u);
             phase1(c1, w);
-            w.minfo = c.take<uint32_t>(T);
-            w.pairs = c.take<uint8_t>(T * kInlinePairs * psz);
+            w.pairs = (v4u32*)c.take<uint8_t>(T * rec_bytes(wide));
             w.ovf_off = c.take<uint32_t>(T);
             w.ovf = c.take<uint8_t>(ovf_cap * psz);
             w.ovf_cap = ovf_cap;
@@ -216,17 +215,15 @@ static int encode_pass(Ctx* ctx, const Derived& d, const uint8_t* d_in, const ui
         if (dump) {
             dump->wide = wide;
             dump->stride = (uint32_t)stride;
-            dump->minfo.resize(total);
             dump->ovf_off.resize(total);
-            dump->pairs.resize(total * kInlinePairs * psz);
+            dump->recs.resize(total * rec_bytes(wide));
             unsigned long long used = 0;
             HIPCHK(hipMemcpyAsync(&used, w.ovf_used, sizeof used, hipMemcpyDeviceToHost, st));
             HIPCHK(hipStreamSynchronize(st));
             dump->ovf.resize(std::min<uint64_t>(used * stride, ovf_cap) * psz);
             if (total) {
-                HIPCHK(hipMemcpyAsync(dump->minfo.data(), w.minfo, total * 4, hipMemcpyDeviceToHost, st));
                 HIPCHK(hipMemcpyAsync(dump->ovf_off.data(), w.ovf_off, total * 4, hipMemcpyDeviceToHost, st));
-                HIPCHK(hipMemcpyAsync(dump->pairs.data(), w.pairs, dump->pairs.size(), hipMemcpyDeviceToHost, st));
+                HIPCHK(hipMemcpyAsync(dump->recs.data(), w.pairs, dump->recs.size(), hipMemcpyDeviceToHost, st));
             }
             if (!dump->ovf.empty()) HIPCHK(hipMemcpyAsync(dump->ovf.data(), w.ovf, dump->ovf.size(), hipMemcpyDeviceToHost, st));
             HIPCHK(hipStreamSynchronize(st));
@@ -234,7 +231,7 @@ static int encode_pass(Ctx* ctx, const Derived& d, const uint8_t* d_in, const ui
         }
         EncArgs a{};
         a.in = inpad; a.offs = d_offs; a.order = d_order; a.nstreams = ns; a.next = d_next;
-        a.minfo = w.minfo; a.pairs = w.pairs; a.ovf_off = w.ovf_off; a.ovf = w.ovf;
+        a.pairs = w.pairs; a.ovf_off = w.ovf_off; a.ovf = w.ovf;
         a.recs = d_recs; a.rec_offs = d_rofs; a.rec_lens = d_rlens; a.out_lens = d_lens; a.status = d_status;
         a.scratch = d_scr; a.scratch_stride = scr;
         a.lit_stride = (enc_lit_bytes(d) + 255) & ~(size_t)255;
@@ -570,22 +567,29 @@ int lzma_match_lists(lzma_ctx* ctx, const lzma_params* p, const uint8_t* in, con
     hipFree(d_in);
     if (rc) return rc;
     uint64_t k = 0;
+    const uint32_t rb = rec_bytes(dump.wide), psz = dump.wide ? 8 : 4;
     for (uint64_t g = 0; g < total; g++) {
-        const uint32_t info = dump.minfo[g], cnt = info & 0xFFFFu;
+        const uint8_t* rec = &dump.recs[g * rb];
+        uint32_t info;
+        memcpy(&info, rec + rb - 16, 4);   // the record's last vector
+        const uint32_t cnt = info & 0xFFFFu;
         counts[g] = cnt;
         main_len[g] = info >> 16;
         for (uint32_t j = 0; j < cnt; j++, k++) {
             uint64_t pr;
-            const uint64_t idx = j < (uint32_t)kInlinePairs ? g * kInlinePairs + j
-                                                            : (uint64_t)dump.ovf_off[g] * dump.stride + j - kInlinePairs;
-            const std::vector<uint8_t>& src = j < (uint32_t)kInlinePairs ? dump.pairs : dump.ovf;
+            const uint8_t* src;
+            if (j < (uint32_t)kInlinePairs) {
+                src = rec + j * psz;
+            } else {
+                const uint64_t idx = (uint64_t)dump.ovf_off[g] * dump.stride + j - kInlinePairs;
+                if ((idx + 1) * psz > dump.ovf.size()) return ctx->fail(LZMA_E_INTERNAL, "pair index out of range");
+                src = &dump.ovf[idx * psz];
+            }
             if (dump.wide) {
-                if ((idx + 1) * 8 > src.size()) return ctx->fail(LZMA_E_INTERNAL, "pair index out of range");
-                memcpy(&pr, &src[idx * 8], 8);
+                memcpy(&pr, src, 8);
             } else {
                 uint32_t v;
-                if ((idx + 1) * 4 > src.size()) return ctx->fail(LZMA_E_INTERNAL, "pair index out of range");
-                memcpy(&v, &src[idx * 4], 4);
+                memcpy(&v, src, 4);
                 pr = ((uint64_t)(v >> 23) << 32) | (v & 0x7FFFFFu);
             }
             if (k < cap && lens && dists) { lens[k] = (uint32_t)(pr >> 32); dists[k] = (uint32_t)pr; }
