@@ -432,6 +432,10 @@ __global__ void __launch_bounds__(64) mf_walk_kernel(const uint8_t* __restrict__
         }
         WNode nd = head;                    // the first node visited is the previous member
         uint32_t count = cut;
+        // direction of the previous step (0 none, 1 ptr0 side, 2 ptr1 side): a step that
+        // goes the same way stores into the very slot it was reached through, which
+        // already holds this node -- the store is skipped (no write, no vmcnt entry)
+        uint32_t prev_dir = 0;
         for (;;) {   // BinTree.java:230-270
             if (cur_match <= match_min || count-- == 0) { put0(0); put1(0); break; }
             uint32_t delta = pos - cur_match;
@@ -454,8 +458,8 @@ __global__ void __launch_bounds__(64) mf_walk_kernel(const uint8_t* __restrict__
             const uint64_t nxt = pby_less ? nd.s1 : nd.s0;
             uint64_t* const here = pby_less ? &nodes[cur_idx].s1 : &nodes[cur_idx].s0;
             if (nxt != 0) nd = nodes[(uint32_t)nxt - 1];   // issued before this step's stores
-            if (pby_less) { put1(node); ptr1 = here; p1_self = false; len1 = len; }
-            else { put0(node); ptr0 = here; p0_self = false; len0 = len; }
+            if (pby_less) { if (prev_dir != 2) put1(node); ptr1 = here; p1_self = false; len1 = len; prev_dir = 2; }
+            else { if (prev_dir != 1) put0(node); ptr0 = here; p0_self = false; len0 = len; prev_dir = 1; }
             if (emit_now) emit(len, delta - 1);
             if (nxt == 0) cur_match = 0;
             else { cur_idx = (uint32_t)nxt - 1; cur_match = (uint32_t)(nxt >> 32); }
