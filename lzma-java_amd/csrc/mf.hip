@@ -437,7 +437,13 @@ __global__ void __launch_bounds__(64) mf_walk_kernel(const uint8_t* __restrict__
         // already holds this node -- the store is skipped (no write, no vmcnt entry)
         uint32_t prev_dir = 0;
         for (;;) {   // BinTree.java:230-270
-            if (cur_match <= match_min || count-- == 0) { put0(0); put1(0); break; }
+            if (cur_match <= match_min || count-- == 0) {
+                // reached through a null link (nxt == 0): that slot already holds 0
+                const bool null_in = cur_match == 0 && prev_dir != 0;
+                if (!(null_in && prev_dir == 1)) put0(0);
+                if (!(null_in && prev_dir == 2)) put1(0);
+                break;
+            }
             uint32_t delta = pos - cur_match;
             uint32_t len = len0 < len1 ? len0 : len1;
             // BinTree.java:243-248: the bytes equal at len => extend; the direction
