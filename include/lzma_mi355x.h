@@ -93,14 +93,32 @@ int lzma_pack_dev(lzma_ctx *ctx, const uint8_t *d_src, const uint64_t *h_src_off
 int lzma_enc_batch(lzma_ctx *ctx, const lzma_params *p,
                    const uint8_t *in, const uint64_t *offs, int nstreams,
                    uint8_t *out, uint64_t out_cap, uint64_t *out_offs);
-/* One stream: Encoder.Code(in, out, -1, -1, null). */
+/* One stream: Encoder.Code(in, out, -1, -1, null).
+ * Stream length: every stream must be shorter than 2^31 bytes (LZMA_E_PARAM
+ * otherwise). This is an API departure from Encoder.Code, which accepts any
+ * length and renormalises positions at 2^30 - 1 (BinTree.java:19, 88-90,
+ * 358-375) without changing any output bit: the device keeps 32-bit positions
+ * and about 100 bytes of workspace per input byte.
+ * Longer inputs are encoded as independent streams. */
 int lzma_encode(lzma_ctx *ctx, const lzma_params *p, const uint8_t *in, uint64_t n,
                 uint8_t *out, uint64_t out_cap, uint64_t *out_len);
 
 /* ---- decode -------------------------------------------------------------
  * props: the 5 property bytes (Decoder.SetDecoderProperties).
  * h_out_sizes[i] = outSize of Decoder.Code (-1 => until end marker).
- * h_status[i] = LZMA_OK, LZMA_E_DATA (Decoder.Code false) or LZMA_E_OVERFLOW. */
+ * h_status[i] = LZMA_OK, LZMA_E_DATA (Decoder.Code false) or LZMA_E_OVERFLOW.
+ * h_out_lens[i] = bytes decoded. As in Decoder.Code, a match may run past
+ * outSize (CopyBlock copies whole matches, OutWindow.java:53-67), so a region
+ * needs outSize + 273 bytes of capacity to never report LZMA_E_OVERFLOW.
+ * On LZMA_E_DATA the region holds every byte decoded before the corrupt
+ * symbol; the reference's OutputStream has by then received only the whole
+ * windows OutWindow flushed (OutWindow.java:63-73, window = max(dict, 4096),
+ * Decoder.java:167), i.e. the first floor(len / window) * window bytes.
+ * lzma_visible_on_error() gives that prefix length; the drop-ins write it.
+ * Input is consumed whole: the reference's RangeDecoder reads its stream
+ * lazily (RangeDecoder.java:19-25) and leaves bytes past the stream unread,
+ * a departure the drop-in handles with mark/reset where the stream allows. */
+uint64_t lzma_visible_on_error(uint32_t dict_size, uint64_t decoded_len);
 int lzma_dec_batch_dev(lzma_ctx *ctx, const uint8_t props[5],
                        const uint8_t *d_in, const uint64_t *h_in_offs, int nstreams,
                        const int64_t *h_out_sizes,
@@ -125,6 +143,9 @@ int lzma_mctx_create(uint32_t device_mask, lzma_mctx **out);
 void lzma_mctx_destroy(lzma_mctx *m);
 const char *lzma_mctx_last_error(const lzma_mctx *m);
 int lzma_mctx_devices(const lzma_mctx *m);
+/* lzma_ctx_set_batch_bytes / lzma_ctx_set_timing applied to every device's context. */
+int lzma_mctx_set_batch_bytes(lzma_mctx *m, uint64_t bytes);
+int lzma_mctx_set_timing(lzma_mctx *m, int on);
 int lzma_enc_batch_multi(lzma_mctx *m, const lzma_params *p, const uint8_t *in, const uint64_t *offs, int nstreams,
                          uint8_t *out, uint64_t out_cap, uint64_t *out_offs);
 int lzma_dec_batch_multi(lzma_mctx *m, const uint8_t props[5], const uint8_t *in, const uint64_t *in_offs,

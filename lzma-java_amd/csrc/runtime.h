@@ -61,8 +61,39 @@ struct TimedLaunch {
     ~TimedLaunch();
 };
 
+// Handle tags: every C entry point checks the tag of the handle it is given, so an
+// lzma_mctx* (multi.hip) passed where an lzma_ctx* is expected is rejected with
+// LZMA_E_PARAM instead of being written through.
+constexpr uint32_t kCtxMagic = 0x58435A4Cu;    // "LZCX"
+constexpr uint32_t kMctxMagic = 0x584D5A4Cu;   // "LZMX" (multi.hip)
+
+// A device buffer that grows on demand and is kept for the context's lifetime, so
+// repeated host-buffer calls (the JNI single-stream path) allocate nothing per call.
+struct DevBuf {
+    void* p = nullptr;
+    size_t n = 0;
+    bool ensure(size_t want) {
+        if (want <= n) return true;
+        if (p) hipFree(p);
+        p = nullptr;
+        n = 0;
+        if (hipMalloc(&p, want) != hipSuccess) return false;
+        n = want;
+        return true;
+    }
+    void release() {
+        if (p) hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+    template <typename T> T* as() const { return (T*)p; }
+};
+
 struct Ctx {
+    uint32_t magic = kCtxMagic;   // first member: see kCtxMagic
     int device = 0;
+    // host-buffer entry points (lzma_enc_batch, lzma_dec_batch, lzma_match_lists): staging in HBM
+    DevBuf io_in, io_out, io_pack, io_offs;
     std::string err;
     bool debug = getenv("LZMA_MI355X_DEBUG") != nullptr;   // phase trace on stderr (synchronises)
     uint64_t batch_bytes = 512ull << 20;

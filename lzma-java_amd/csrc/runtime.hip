@@ -9,6 +9,7 @@
 // would compute returns LZMA_E_NODEVICE.
 #include <algorithm>
 #include <cstring>
+#include <new>
 #include <numeric>
 #include <vector>
 
@@ -30,6 +31,8 @@ __global__ void pack_kernel(const uint8_t* __restrict__ src, const uint64_t* __r
         for (uint64_t i = threadIdx.x; i < len; i += blockDim.x) dst[o + i] = src[a + i];
     }
 }
+
+static bool ok_ctx(const Ctx* c) { return c && c->magic == kCtxMagic; }
 
 static int check_device(Ctx* ctx) {
     int n = 0;
@@ -405,45 +408,54 @@ int lzma_read_props(const uint8_t in[5], lzma_params* p) {   // Decoder.java:303
 
 uint64_t lzma_enc_bound(uint64_t n) { return n + n / 8 + 4096; }
 
+uint64_t lzma_visible_on_error(uint32_t dict_size, uint64_t decoded_len) {   // OutWindow.Flush at whole windows
+    const uint64_t dict = (int32_t)dict_size < 1 ? 1 : dict_size;                // Decoder.SetDictionarySize :160-170
+    const uint64_t w = dict > 4096 ? dict : 4096;                                // Decoder.java:167
+    return decoded_len / w * w;
+}
+
 int lzma_ctx_create(int device, lzma_ctx** out) {
     if (!out) return LZMA_E_PARAM;
     *out = nullptr;
     int rc = check_device(nullptr);
     if (rc) return rc;
     if (hipSetDevice(device) != hipSuccess) return LZMA_E_DEVICE;
-    lzma_ctx* c = new lzma_ctx();
+    lzma_ctx* c = new (std::nothrow) lzma_ctx();
+    if (!c) return LZMA_E_NOMEM;
     c->device = device;
     *out = c;
     return LZMA_OK;
 }
 
 void lzma_ctx_destroy(lzma_ctx* ctx) {
-    if (!ctx) return;
+    if (!ok_ctx(ctx)) return;
     hipSetDevice(ctx->device);
     ctx->resolve_timings();
     for (auto e : ctx->free_events) hipEventDestroy(e);
     if (ctx->arena) hipFree(ctx->arena);
     if (ctx->litbuf) hipFree(ctx->litbuf);
     if (ctx->tmp) hipFree(ctx->tmp);
+    ctx->io_in.release(); ctx->io_out.release(); ctx->io_pack.release(); ctx->io_offs.release();
+    ctx->magic = 0;
     delete ctx;
 }
 
-const char* lzma_last_error(const lzma_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+const char* lzma_last_error(const lzma_ctx* ctx) { return ok_ctx(ctx) ? ctx->err.c_str() : "null or invalid context"; }
 
 int lzma_ctx_set_batch_bytes(lzma_ctx* ctx, uint64_t bytes) {
-    if (!ctx || bytes < 4096) return LZMA_E_PARAM;
+    if (!ok_ctx(ctx) || bytes < 4096) return LZMA_E_PARAM;
     ctx->batch_bytes = bytes;
     return LZMA_OK;
 }
 
 int lzma_ctx_set_timing(lzma_ctx* ctx, int on) {
-    if (!ctx) return LZMA_E_PARAM;
+    if (!ok_ctx(ctx)) return LZMA_E_PARAM;
     ctx->timing = on != 0;
     return LZMA_OK;
 }
 
 int lzma_ctx_timings(lzma_ctx* ctx, const char** names, double* ms, int64_t* launches, int cap) {
-    if (!ctx) return LZMA_E_PARAM;
+    if (!ok_ctx(ctx)) return LZMA_E_PARAM;
     hipSetDevice(ctx->device);
     ctx->resolve_timings();
     int i = 0;
@@ -458,14 +470,14 @@ int lzma_ctx_timings(lzma_ctx* ctx, const char** names, double* ms, int64_t* lau
 }
 
 void lzma_ctx_reset_timings(lzma_ctx* ctx) {
-    if (!ctx) return;
+    if (!ok_ctx(ctx)) return;
     ctx->resolve_timings();
     ctx->acc.clear();
 }
 
 int lzma_enc_batch_dev(lzma_ctx* ctx, const lzma_params* p, const uint8_t* d_in, const uint64_t* h_offs, int nstreams,
                        uint8_t* d_out, const uint64_t* h_out_offs, uint64_t* h_out_lens, void* hip_stream) {
-    if (!ctx || !p || !h_offs || !h_out_offs || !h_out_lens) return LZMA_E_PARAM;
+    if (!ok_ctx(ctx) || !p || !h_offs || !h_out_offs || !h_out_lens) return LZMA_E_PARAM;
     if (check_device(ctx)) return LZMA_E_NODEVICE;
     hipSetDevice(ctx->device);
     return encode_batch_dev(ctx, p, d_in, h_offs, nstreams, d_out, h_out_offs, h_out_lens, (hipStream_t)hip_stream);
@@ -473,7 +485,7 @@ int lzma_enc_batch_dev(lzma_ctx* ctx, const lzma_params* p, const uint8_t* d_in,
 
 int lzma_pack_dev(lzma_ctx* ctx, const uint8_t* d_src, const uint64_t* h_src_offs, const uint64_t* h_lens, int nstreams,
                   uint8_t* d_dst, const uint64_t* h_dst_offs, void* hip_stream) {
-    if (!ctx || !h_src_offs || !h_lens || !h_dst_offs || nstreams < 0) return LZMA_E_PARAM;
+    if (!ok_ctx(ctx) || !h_src_offs || !h_lens || !h_dst_offs || nstreams < 0) return LZMA_E_PARAM;
     if (check_device(ctx)) return LZMA_E_NODEVICE;
     if (nstreams == 0) return LZMA_OK;
     hipSetDevice(ctx->device);
@@ -500,47 +512,47 @@ int lzma_pack_dev(lzma_ctx* ctx, const uint8_t* d_src, const uint64_t* h_src_off
 
 int lzma_enc_batch(lzma_ctx* ctx, const lzma_params* p, const uint8_t* in, const uint64_t* offs, int nstreams,
                    uint8_t* out, uint64_t out_cap, uint64_t* out_offs) {
-    if (!ctx || !p || !offs || !out_offs || nstreams < 0) return LZMA_E_PARAM;
+    if (!ok_ctx(ctx) || !p || !offs || !out_offs || nstreams < 0) return LZMA_E_PARAM;
     if (check_device(ctx)) return LZMA_E_NODEVICE;
     hipSetDevice(ctx->device);
     Derived d;
     if (derive(*p, d) != LZMA_OK) return ctx->fail(LZMA_E_PARAM, "invalid lzma_params");
     const uint64_t total = offs[nstreams] - offs[0];
-    std::vector<uint64_t> rel(nstreams + 1), cap_offs(nstreams + 1), lens(nstreams);
+    std::vector<uint64_t> rel(nstreams + 1), cap_offs(nstreams + 1), lens(nstreams), pack(nstreams + 1);
     cap_offs[0] = 0;
     for (int i = 0; i <= nstreams; i++) rel[i] = offs[i] - offs[0];
     for (int i = 0; i < nstreams; i++) cap_offs[i + 1] = cap_offs[i] + lzma_enc_bound(rel[i + 1] - rel[i]);
-    uint8_t *d_in = nullptr, *d_out = nullptr, *d_pack = nullptr;
-    uint64_t *d_co = nullptr, *d_po = nullptr;
-    int rc = LZMA_OK;
-    std::vector<uint64_t> pack(nstreams + 1);
+    // staging buffers persist in the context (grown, never shrunk): no hipMalloc per call
+    if (!ctx->io_in.ensure(total + 1) || !ctx->io_out.ensure(cap_offs[nstreams] + 1) ||
+        !ctx->io_offs.ensure(16 * ((size_t)nstreams + 1)))
+        return ctx->fail(LZMA_E_NOMEM, "device staging buffers");
+    uint8_t* d_in = ctx->io_in.as<uint8_t>();
+    uint8_t* d_out = ctx->io_out.as<uint8_t>();
+    uint64_t* d_co = ctx->io_offs.as<uint64_t>();
+    uint64_t* d_po = d_co + nstreams + 1;
     hipStream_t st = nullptr;
-    if (hipMalloc(&d_in, total + 1) != hipSuccess || hipMalloc(&d_out, cap_offs[nstreams] + 1) != hipSuccess) {
-        rc = ctx->fail(LZMA_E_NOMEM, "device buffers");
-        goto done;
-    }
-    if (total && hipMemcpy(d_in, in + offs[0], total, hipMemcpyHostToDevice) != hipSuccess) { rc = ctx->fail(LZMA_E_DEVICE, "H2D"); goto done; }
-    rc = encode_batch_dev(ctx, p, d_in, rel.data(), nstreams, d_out, cap_offs.data(), lens.data(), st);
-    if (rc) goto done;
+    if (total) HIPCHK(hipMemcpy(d_in, in + offs[0], total, hipMemcpyHostToDevice));
+    int rc = encode_batch_dev(ctx, p, d_in, rel.data(), nstreams, d_out, cap_offs.data(), lens.data(), st);
+    if (rc) return rc;
     pack[0] = 0;
     for (int i = 0; i < nstreams; i++) pack[i + 1] = pack[i] + lens[i];
-    if (pack[nstreams] > out_cap) { rc = ctx->fail(LZMA_E_OVERFLOW, "out_cap %llu < %llu", (unsigned long long)out_cap, (unsigned long long)pack[nstreams]); goto done; }
-    if (hipMalloc(&d_pack, pack[nstreams] + 1) != hipSuccess || hipMalloc(&d_co, (nstreams + 1) * 8) != hipSuccess ||
-        hipMalloc(&d_po, (nstreams + 1) * 8) != hipSuccess) { rc = ctx->fail(LZMA_E_NOMEM, "pack buffers"); goto done; }
-    hipMemcpy(d_co, cap_offs.data(), (nstreams + 1) * 8, hipMemcpyHostToDevice);
-    hipMemcpy(d_po, pack.data(), (nstreams + 1) * 8, hipMemcpyHostToDevice);
+    if (pack[nstreams] > out_cap)
+        return ctx->fail(LZMA_E_OVERFLOW, "out_cap %llu < %llu", (unsigned long long)out_cap, (unsigned long long)pack[nstreams]);
+    if (!ctx->io_pack.ensure(pack[nstreams] + 1)) return ctx->fail(LZMA_E_NOMEM, "pack buffer");
+    uint8_t* d_pack = ctx->io_pack.as<uint8_t>();
+    HIPCHK(hipMemcpy(d_co, cap_offs.data(), (nstreams + 1) * 8, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(d_po, pack.data(), (nstreams + 1) * 8, hipMemcpyHostToDevice));
     if (nstreams > 0) hipLaunchKernelGGL(pack_kernel, dim3(std::min(nstreams, 65535)), dim3(256), 0, st, d_out, d_co, d_po, d_pack, nstreams);
-    if (pack[nstreams] && hipMemcpy(out, d_pack, pack[nstreams], hipMemcpyDeviceToHost) != hipSuccess) { rc = ctx->fail(LZMA_E_DEVICE, "D2H"); goto done; }
+    HIPCHK(hipGetLastError());
+    if (pack[nstreams]) HIPCHK(hipMemcpy(out, d_pack, pack[nstreams], hipMemcpyDeviceToHost));
     for (int i = 0; i <= nstreams; i++) out_offs[i] = pack[i];
-done:
-    hipFree(d_in); hipFree(d_out); hipFree(d_pack); hipFree(d_co); hipFree(d_po);
-    return rc;
+    return LZMA_OK;
 }
 
 int lzma_match_lists(lzma_ctx* ctx, const lzma_params* p, const uint8_t* in, const uint64_t* offs, int nstreams,
                      uint32_t* counts, uint32_t* main_len, uint32_t* lens, uint32_t* dists, uint64_t cap,
                      uint64_t* total_pairs) {
-    if (!ctx || !p || !offs || nstreams < 0 || !counts || !main_len || !total_pairs) return LZMA_E_PARAM;
+    if (!ok_ctx(ctx) || !p || !offs || nstreams < 0 || !counts || !main_len || !total_pairs) return LZMA_E_PARAM;
     if (check_device(ctx)) return LZMA_E_NODEVICE;
     hipSetDevice(ctx->device);
     Derived d;
@@ -549,22 +561,22 @@ int lzma_match_lists(lzma_ctx* ctx, const lzma_params* p, const uint8_t* in, con
     if (nstreams == 0) return LZMA_OK;
     const uint64_t total = offs[nstreams] - offs[0];
     if (total >= (1ull << 31)) return ctx->fail(LZMA_E_PARAM, "match-list dump is limited to one pass (< 2 GiB)");
+    // one pass: the match finder's 32-bit hash2/hash3 sort keys hold the stream index in the bits above the
+    // hash (runtime.h MfArgs), valid for at most kMaxStreamsPerPass streams
+    if (nstreams > kMaxStreamsPerPass)
+        return ctx->fail(LZMA_E_PARAM, "match-list dump is limited to %d streams per call", kMaxStreamsPerPass);
     std::vector<uint64_t> rel(nstreams + 1), oo(nstreams + 1, 0), lens_h(nstreams);
     std::vector<int32_t> status(nstreams);
     for (int i = 0; i <= nstreams; i++) {
         rel[i] = offs[i] - offs[0];
         if (i && rel[i] < rel[i - 1]) return ctx->fail(LZMA_E_PARAM, "offsets not monotone");
     }
-    uint8_t* d_in = nullptr;
-    if (hipMalloc(&d_in, total + 1) != hipSuccess) return ctx->fail(LZMA_E_NOMEM, "device input");
-    if (total && hipMemcpy(d_in, in + offs[0], total, hipMemcpyHostToDevice) != hipSuccess) {
-        hipFree(d_in);
-        return ctx->fail(LZMA_E_DEVICE, "H2D");
-    }
+    if (!ctx->io_in.ensure(total + 1)) return ctx->fail(LZMA_E_NOMEM, "device input");
+    uint8_t* d_in = ctx->io_in.as<uint8_t>();
+    if (total) HIPCHK(hipMemcpy(d_in, in + offs[0], total, hipMemcpyHostToDevice));
     MatchDump dump;
     int rc = encode_pass(ctx, d, d_in, rel.data(), 0, nstreams, nullptr, oo.data(), lens_h.data(), status.data(),
                          nullptr, &dump);
-    hipFree(d_in);
     if (rc) return rc;
     uint64_t k = 0;
     const uint32_t rb = rec_bytes(dump.wide), psz = dump.wide ? 8 : 4;
@@ -611,7 +623,7 @@ int lzma_encode(lzma_ctx* ctx, const lzma_params* p, const uint8_t* in, uint64_t
 int lzma_dec_batch_dev(lzma_ctx* ctx, const uint8_t props[5], const uint8_t* d_in, const uint64_t* h_in_offs, int nstreams,
                        const int64_t* h_out_sizes, uint8_t* d_out, const uint64_t* h_out_offs, uint64_t* h_out_lens,
                        int32_t* h_status, void* hip_stream) {
-    if (!ctx || !props || !h_in_offs || !h_out_sizes || !h_out_offs || !h_out_lens || !h_status) return LZMA_E_PARAM;
+    if (!ok_ctx(ctx) || !props || !h_in_offs || !h_out_sizes || !h_out_offs || !h_out_lens || !h_status) return LZMA_E_PARAM;
     if (check_device(ctx)) return LZMA_E_NODEVICE;
     hipSetDevice(ctx->device);
     return decode_batch_dev(ctx, props, d_in, h_in_offs, nstreams, h_out_sizes, d_out, h_out_offs, h_out_lens, h_status,
@@ -620,29 +632,29 @@ int lzma_dec_batch_dev(lzma_ctx* ctx, const uint8_t props[5], const uint8_t* d_i
 
 int lzma_dec_batch(lzma_ctx* ctx, const uint8_t props[5], const uint8_t* in, const uint64_t* in_offs, int nstreams,
                    const int64_t* out_sizes, uint8_t* out, const uint64_t* out_offs, uint64_t* out_lens, int32_t* status) {
-    if (!ctx || !props || !in_offs || !out_sizes || !out_offs || !out_lens || !status || nstreams < 0) return LZMA_E_PARAM;
+    if (!ok_ctx(ctx) || !props || !in_offs || !out_sizes || !out_offs || !out_lens || !status || nstreams < 0) return LZMA_E_PARAM;
     if (check_device(ctx)) return LZMA_E_NODEVICE;
     hipSetDevice(ctx->device);
     const uint64_t tin = in_offs[nstreams] - in_offs[0];
     const uint64_t tout = out_offs[nstreams] - out_offs[0];
     std::vector<uint64_t> rin(nstreams + 1), rout(nstreams + 1);
     for (int i = 0; i <= nstreams; i++) { rin[i] = in_offs[i] - in_offs[0]; rout[i] = out_offs[i] - out_offs[0]; }
-    uint8_t *d_in = nullptr, *d_out = nullptr;
-    int rc = LZMA_OK;
-    if (hipMalloc(&d_in, tin + 1) != hipSuccess || hipMalloc(&d_out, tout + 1) != hipSuccess) {
-        rc = ctx->fail(LZMA_E_NOMEM, "device buffers");
-    } else {
-        if (tin) hipMemcpy(d_in, in + in_offs[0], tin, hipMemcpyHostToDevice);
-        rc = decode_batch_dev(ctx, props, d_in, rin.data(), nstreams, out_sizes, d_out, rout.data(), out_lens, status, nullptr);
-        if (rc == LZMA_OK && tout) {
+    // staging buffers persist in the context (grown, never shrunk): no hipMalloc per call
+    if (!ctx->io_in.ensure(tin + 1) || !ctx->io_out.ensure(tout + 1)) return ctx->fail(LZMA_E_NOMEM, "device buffers");
+    uint8_t* d_in = ctx->io_in.as<uint8_t>();
+    uint8_t* d_out = ctx->io_out.as<uint8_t>();
+    if (tin) HIPCHK(hipMemcpy(d_in, in + in_offs[0], tin, hipMemcpyHostToDevice));
+    int rc = decode_batch_dev(ctx, props, d_in, rin.data(), nstreams, out_sizes, d_out, rout.data(), out_lens, status, nullptr);
+    if (rc == LZMA_OK && tout) {
+        if (nstreams > 16) {   // one copy of the whole layout (bytes past a stream's length are capacity)
+            HIPCHK(hipMemcpy(out + out_offs[0], d_out, tout, hipMemcpyDeviceToHost));
+        } else {
             for (int i = 0; i < nstreams; i++) {
                 uint64_t L = std::min<uint64_t>(out_lens[i], rout[i + 1] - rout[i]);
-                if (L) hipMemcpy(out + out_offs[i], d_out + rout[i], L, hipMemcpyDeviceToHost);
+                if (L) HIPCHK(hipMemcpy(out + out_offs[i], d_out + rout[i], L, hipMemcpyDeviceToHost));
             }
         }
     }
-    hipFree(d_in);
-    hipFree(d_out);
     return rc;
 }
 

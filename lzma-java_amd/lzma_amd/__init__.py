@@ -43,7 +43,8 @@ EXPORTED_SYMBOLS = [
     "lzma_encode", "lzma_dec_batch_dev", "lzma_dec_batch", "lzma_decode", "lzma_bench_generate",
     "lzma_rnd_generate", "lzma_text_generate", "lzma_match_lists",
     "lzma_mctx_create", "lzma_mctx_destroy", "lzma_mctx_last_error", "lzma_mctx_devices",
-    "lzma_enc_batch_multi", "lzma_dec_batch_multi",
+    "lzma_enc_batch_multi", "lzma_dec_batch_multi", "lzma_mctx_set_batch_bytes", "lzma_mctx_set_timing",
+    "lzma_visible_on_error",
 ]
 
 
@@ -112,6 +113,10 @@ def lib():
         L.lzma_mctx_last_error.argtypes = [vp]
         L.lzma_mctx_last_error.restype = ctypes.c_char_p
         L.lzma_mctx_devices.argtypes = [vp]
+        L.lzma_mctx_set_batch_bytes.argtypes = [vp, u64]
+        L.lzma_mctx_set_timing.argtypes = [vp, i32]
+        L.lzma_visible_on_error.argtypes = [ctypes.c_uint32, u64]
+        L.lzma_visible_on_error.restype = u64
         L.lzma_enc_batch_multi.argtypes = [vp, P, vp, vp, i32, vp, u64, vp]
         L.lzma_dec_batch_multi.argtypes = [vp, vp, vp, vp, i32, vp, vp, vp, vp, vp]
         L.lzma_match_lists.argtypes = [vp, P, vp, vp, i32, vp, vp, vp, vp, u64, ctypes.POINTER(u64)]
@@ -155,6 +160,12 @@ def read_props(props: bytes) -> Optional[Params]:
 
 def enc_bound(n: int) -> int:
     return int(lib().lzma_enc_bound(n))
+
+
+def visible_on_error(dict_size: int, decoded_len: int) -> int:
+    """Bytes Decoder.Code has written when it returns false after decoding
+    decoded_len bytes: the whole windows OutWindow flushed (lzma_visible_on_error)."""
+    return int(lib().lzma_visible_on_error(dict_size & 0xFFFFFFFF, decoded_len))
 
 
 def bench_generate(size: int) -> np.ndarray:
@@ -334,9 +345,13 @@ class Context:
         return lens[:n], status[:n]
 
 
-class MultiContext(Context):
+class MultiContext:
     """Several devices from one process (lzma_mctx, SURVEY 8(b) device_mask):
-    the batch calls deal the streams round-robin over the devices in the mask."""
+    the batch calls deal the streams round-robin over the devices in the mask.
+
+    Not a Context subclass: an lzma_mctx handle is not an lzma_ctx, so only the
+    operations the multi-device C entry points provide exist here (the C side
+    also rejects a handle of the wrong kind with LZMA_E_PARAM)."""
 
     def __init__(self, device_mask: int):
         h = ctypes.c_void_p()
@@ -352,8 +367,24 @@ class MultiContext(Context):
             lib().lzma_mctx_destroy(self.h)
             self.h = None
 
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
     def error(self) -> str:
         return lib().lzma_mctx_last_error(self.h).decode()
+
+    def check(self, rc):
+        if rc != LZMA_OK:
+            raise LzmaError(rc, self.error())
+
+    def set_batch_bytes(self, n: int):
+        self.check(lib().lzma_mctx_set_batch_bytes(self.h, n))
+
+    def set_timing(self, on: bool):
+        self.check(lib().lzma_mctx_set_timing(self.h, 1 if on else 0))
 
     def encode_batch(self, streams: Sequence[bytes], p: Params) -> List[bytes]:
         arrs = [np.frombuffer(s, dtype=np.uint8) if not isinstance(s, np.ndarray) else s for s in streams]
@@ -508,6 +539,11 @@ class Decoder:
                 cap *= 4
                 continue
             break
+        if st != LZMA_OK:
+            # Code returns false with only the whole windows OutWindow flushed so far
+            # written (OutWindow.java:63-73; window = max(dict, 4096), Decoder.java:167)
+            dict_size = int.from_bytes(self._props[1:5], "little")
+            out = out[:visible_on_error(dict_size, len(out))]
         outStream.write(out)
         return st == LZMA_OK
 

@@ -141,3 +141,42 @@ def test_no_device_fails_loudly():
     assert ei.value.code == lzma_amd.LZMA_E_NODEVICE
     with pytest.raises(lzma_amd.LzmaError):
         lzma_amd.Encoder().Code(b"abc", __import__("io").BytesIO())
+
+
+def _fake_handle(magic):
+    buf = ctypes.create_string_buffer(512)
+    ctypes.memmove(buf, ctypes.c_uint32(magic).value.to_bytes(4, "little"), 4)
+    return buf
+
+
+def test_handles_of_the_wrong_kind_are_rejected():
+    # an lzma_mctx* passed where an lzma_ctx* is expected (and the
+    # reverse) must be refused with LZMA_E_PARAM, never written through
+    L = lzma_amd.lib()
+    mctx_like, ctx_like, junk = _fake_handle(0x584D5A4C), _fake_handle(0x58435A4C), _fake_handle(0)
+    for h in (mctx_like, junk):
+        assert L.lzma_ctx_set_batch_bytes(h, 1 << 30) == lzma_amd.LZMA_E_PARAM
+        assert L.lzma_ctx_set_timing(h, 1) == lzma_amd.LZMA_E_PARAM
+        assert L.lzma_ctx_timings(h, None, None, None, 0) == lzma_amd.LZMA_E_PARAM
+        assert b"invalid" in L.lzma_last_error(h)
+        assert bytes(h.raw[4:64]) == b"\0" * 60   # nothing written
+    for h in (ctx_like, junk):
+        assert L.lzma_mctx_set_batch_bytes(h, 1 << 30) == lzma_amd.LZMA_E_PARAM
+        assert L.lzma_mctx_set_timing(h, 1) == lzma_amd.LZMA_E_PARAM
+        assert L.lzma_mctx_devices(h) == 0
+
+
+def test_multicontext_is_not_a_single_device_context():
+    assert not issubclass(lzma_amd.MultiContext, lzma_amd.Context)
+    for name in ("encode_batch_dev", "decode_batch_dev", "pack_dev", "match_lists", "timings"):
+        assert not hasattr(lzma_amd.MultiContext, name), name
+    for name in ("set_batch_bytes", "set_timing", "encode_batch", "decode_batch", "close"):
+        assert hasattr(lzma_amd.MultiContext, name), name
+
+
+@pytest.mark.parametrize("dict_size,n,exp", [(1 << 16, 200000, 196608), (1 << 16, 65535, 0), (1, 10000, 8192),
+                                             (0, 4095, 0), (1 << 20, (1 << 20) + 5, 1 << 20)])
+def test_visible_on_error_is_whole_windows(dict_size, n, exp):
+    # Decoder.Code returning false has written only OutWindow's whole-window flushes
+    # (OutWindow.java:63-73), window = max(dict, 4096) (Decoder.java:166-167)
+    assert lzma_amd.visible_on_error(dict_size, n) == exp
