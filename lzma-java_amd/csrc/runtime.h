@@ -96,6 +96,11 @@ struct Ctx {
     DevBuf io_in, io_out, io_pack, io_offs;
     std::string err;
     bool debug = getenv("LZMA_MI355X_DEBUG") != nullptr;   // phase trace on stderr (synchronises)
+    // parse kernel choice: 0 = by stream count (solo when <= kSoloPerCu per CU), 1 = always the
+    // batch kernel, 2 = always the solo kernel (LZMA_MI355X_ENC=batch|solo; tests cover both)
+    int enc_mode = getenv("LZMA_MI355X_ENC") ? (strcmp(getenv("LZMA_MI355X_ENC"), "batch") == 0 ? 1
+                                                : strcmp(getenv("LZMA_MI355X_ENC"), "solo") == 0 ? 2 : 0) : 0;
+    int cus = 0;                  // compute units of the device (hipDeviceAttributeMultiprocessorCount)
     uint64_t batch_bytes = 512ull << 20;
     // persistent workspace arena (grown, never shrunk)
     uint8_t* arena = nullptr;
@@ -276,6 +281,7 @@ struct EncArgs {
     uint32_t fb, lc, lp, pb, eos, dist_table_size, len_table_size;
     uint32_t lit_in_lds;
     uint32_t pair_bytes;          // 4 (u32 packed pairs) or 8 (u64, streams >= 8 MiB)
+    uint32_t solo;                // 1: the solo kernel (enc.hip enc_kernel_solo), 0: the batch kernel
     uint32_t* dbg;                // debug checkpoints (host-mapped, LZMA_MI355X_DEBUG only) or null
     uint64_t* prof;               // phase cycles [nstreams][kProfSlots] (LZG_PROF builds) or null
 };
@@ -305,7 +311,9 @@ int launch_rc(Ctx* ctx, const RcArgs& a, hipStream_t st);
 // records one stream of n bytes can need: <= 21 per byte (a length-2 match: isMatch, isRep,
 // 4 length bits, 6 slot bits, 30 footer bits), the end marker (42) and the first literal
 __host__ __device__ inline uint64_t rc_record_bound(uint64_t n) { return (24 * n + 64 + 63) & ~(uint64_t)63; }
-uint32_t enc_lit_in_lds(const Derived& d);
+uint32_t enc_lit_in_lds(const Derived& d, bool solo);
+// the solo parse kernel runs when a pass has at most kSoloPerCu streams per CU
+constexpr int kSoloPerCu = 4;
 size_t enc_scratch_per_block(const Derived& d);
 size_t enc_lit_bytes(const Derived& d);
 
