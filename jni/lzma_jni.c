@@ -1,0 +1,157 @@
+/*
+ * lzma_jni.c -- JNI binding of the MI355X LZMA path (include/lzma_mi355x.h) for the
+ * Java drop-in classes in java/SevenZip/Compression/LZMA/ (Encoder, Decoder, Native).
+ *
+ * Replaces, for the Java callers of rfalke/lzma-java, the hot path of
+ *   Encoder.Code   src/main/java/SevenZip/Compression/LZMA/Encoder.java:1064-1077
+ *   Decoder.Code   src/main/java/SevenZip/Compression/LZMA/Decoder.java:205-301
+ * The setters' range checks stay in Java with the reference's return values.
+ *
+ * Build (needs a JDK; none exists in the build container or on the GPU box, so this
+ * file is not compiled by the repository's own build): see jni/Makefile.
+ *
+ * One device context per process on the first device of the mask
+ * -Dlzma.mi355x.devices (default 1 = device 0); encodeBatch deals a batch's streams
+ * over every device of the mask (lzma_enc_batch_multi). The contexts keep their
+ * device buffers between calls (no hipMalloc per Code call). Calls are serialised:
+ * the reference's Encoder/Decoder instances are single-threaded, and so is a context.
+ */
+#include <jni.h>
+#include <pthread.h>
+#include <stdint.h>
+#include <stdlib.h>
+
+#include "lzma_mi355x.h"
+
+static lzma_mctx *g_m;
+static lzma_ctx *g_ctx;
+static pthread_mutex_t g_lock = PTHREAD_MUTEX_INITIALIZER;
+
+static void throw_io(JNIEnv *env, const char *msg) {
+    jclass c = (*env)->FindClass(env, "java/io/IOException");
+    if (c) (*env)->ThrowNew(env, c, msg);
+}
+
+/* static native boolean init(int deviceMask) */
+JNIEXPORT jboolean JNICALL Java_SevenZip_Compression_LZMA_Native_init(JNIEnv *env, jclass cls, jint mask) {
+    (void)env; (void)cls;
+    uint32_t m = mask ? (uint32_t)mask : 1u;
+    pthread_mutex_lock(&g_lock);
+    int ok = g_ctx != NULL;
+    if (!ok && lzma_mctx_create(m, &g_m) == LZMA_OK) {
+        int first = 0;
+        while (!(m >> first & 1u)) first++;
+        ok = lzma_ctx_create(first, &g_ctx) == LZMA_OK;
+    }
+    pthread_mutex_unlock(&g_lock);
+    return ok ? JNI_TRUE : JNI_FALSE;
+}
+
+/* static native byte[] encode(byte[] in, int len, int dict, int fb, int mf, int lc, int lp, int pb,
+ *                             boolean eos): Encoder.Code on in[0..len), the raw stream (no header) */
+JNIEXPORT jbyteArray JNICALL Java_SevenZip_Compression_LZMA_Native_encode(
+        JNIEnv *env, jclass cls, jbyteArray in, jint n, jint dict, jint fb, jint mf,
+        jint lc, jint lp, jint pb, jboolean eos) {
+    (void)cls;
+    lzma_params p = {dict, fb, mf, lc, lp, pb, eos ? 1 : 0};
+    uint64_t cap = lzma_enc_bound((uint64_t)n), len = 0;
+    uint8_t *out = (uint8_t *)malloc(cap);
+    if (!out) { throw_io(env, "out of memory"); return NULL; }
+    jbyte *src = (*env)->GetPrimitiveArrayCritical(env, in, NULL);
+    if (!src) { free(out); return NULL; }
+    pthread_mutex_lock(&g_lock);
+    int rc = lzma_encode(g_ctx, &p, (const uint8_t *)src, (uint64_t)n, out, cap, &len);
+    (*env)->ReleasePrimitiveArrayCritical(env, in, src, JNI_ABORT);
+    if (rc != LZMA_OK) {
+        throw_io(env, lzma_last_error(g_ctx));
+        pthread_mutex_unlock(&g_lock);
+        free(out);
+        return NULL;
+    }
+    pthread_mutex_unlock(&g_lock);
+    jbyteArray r = (*env)->NewByteArray(env, (jsize)len);
+    if (r) (*env)->SetByteArrayRegion(env, r, 0, (jsize)len, (const jbyte *)out);
+    free(out);
+    return r;
+}
+
+/* static native byte[] decode(byte[] props5, byte[] in, int len, long outSize, int[] status):
+ * Decoder.Code on in[0..len). status[0] = LZMA_OK or LZMA_E_DATA (Code returns false).
+ * On LZMA_E_DATA the returned bytes are what the reference had written by then: the whole
+ * windows OutWindow flushed (OutWindow.java:63-73), lzma_visible_on_error. outSize < 0
+ * decodes until the end marker (Decoder.java:219): the output buffer grows on
+ * LZMA_E_OVERFLOW and the stream is decoded again. */
+JNIEXPORT jbyteArray JNICALL Java_SevenZip_Compression_LZMA_Native_decode(
+        JNIEnv *env, jclass cls, jbyteArray props, jbyteArray in, jint n, jlong out_size, jintArray status) {
+    (void)cls;
+    uint8_t pr[5];
+    (*env)->GetByteArrayRegion(env, props, 0, 5, (jbyte *)pr);
+    const uint32_t dict = (uint32_t)pr[1] | ((uint32_t)pr[2] << 8) | ((uint32_t)pr[3] << 16) | ((uint32_t)pr[4] << 24);
+    /* a match may run past outSize (CopyBlock copies whole matches): 273 bytes of slack */
+    uint64_t cap = out_size >= 0 ? (uint64_t)out_size + 273 : (uint64_t)n * 4 + 65536, len = 0;
+    for (;;) {
+        uint8_t *dst = (uint8_t *)malloc(cap ? cap : 1);
+        if (!dst) { throw_io(env, "out of memory"); return NULL; }
+        jbyte *src = (*env)->GetPrimitiveArrayCritical(env, in, NULL);
+        if (!src) { free(dst); return NULL; }
+        pthread_mutex_lock(&g_lock);
+        int rc = lzma_decode(g_ctx, pr, (const uint8_t *)src, (uint64_t)n, (int64_t)out_size, dst, cap, &len);
+        (*env)->ReleasePrimitiveArrayCritical(env, in, src, JNI_ABORT);
+        if (rc == LZMA_E_OVERFLOW && out_size < 0 && cap < ((uint64_t)1 << 31)) {
+            pthread_mutex_unlock(&g_lock);
+            free(dst);
+            cap *= 2;
+            continue;
+        }
+        if (rc != LZMA_OK && rc != LZMA_E_DATA) {
+            throw_io(env, lzma_last_error(g_ctx));
+            pthread_mutex_unlock(&g_lock);
+            free(dst);
+            return NULL;
+        }
+        pthread_mutex_unlock(&g_lock);
+        if (rc == LZMA_E_DATA) len = lzma_visible_on_error(dict, len);
+        jint st = rc;
+        (*env)->SetIntArrayRegion(env, status, 0, 1, &st);
+        jbyteArray r = (*env)->NewByteArray(env, (jsize)len);
+        if (r) (*env)->SetByteArrayRegion(env, r, 0, (jsize)len, (const jbyte *)dst);
+        free(dst);
+        return r;
+    }
+}
+
+/* static native long[] encodeBatch(byte[] in, long[] offs, byte[] out, int dict, int fb, int mf,
+ *                                  int lc, int lp, int pb, boolean eos):
+ * N independent chunks in[offs[i]..offs[i+1]) over the device mask; returns the packed
+ * layout out_offs[N+1] of the encoded streams in out. */
+JNIEXPORT jlongArray JNICALL Java_SevenZip_Compression_LZMA_Native_encodeBatch(
+        JNIEnv *env, jclass cls, jbyteArray in, jlongArray offs, jbyteArray out,
+        jint dict, jint fb, jint mf, jint lc, jint lp, jint pb, jboolean eos) {
+    (void)cls;
+    lzma_params p = {dict, fb, mf, lc, lp, pb, eos ? 1 : 0};
+    jsize n = (*env)->GetArrayLength(env, offs) - 1;
+    if (n < 0) { throw_io(env, "offs must hold N + 1 entries"); return NULL; }
+    uint64_t *oo = (uint64_t *)malloc(sizeof(uint64_t) * ((size_t)n + 1));
+    if (!oo) { throw_io(env, "out of memory"); return NULL; }
+    jlong *o = (*env)->GetLongArrayElements(env, offs, NULL);
+    jbyte *src = (*env)->GetPrimitiveArrayCritical(env, in, NULL);
+    jbyte *dst = (*env)->GetPrimitiveArrayCritical(env, out, NULL);
+    pthread_mutex_lock(&g_lock);
+    int rc = (o && src && dst) ? lzma_enc_batch_multi(g_m, &p, (const uint8_t *)src, (const uint64_t *)o, n, (uint8_t *)dst,
+                                                      (uint64_t)(*env)->GetArrayLength(env, out), oo)
+                               : LZMA_E_NOMEM;
+    if (dst) (*env)->ReleasePrimitiveArrayCritical(env, out, dst, 0);
+    if (src) (*env)->ReleasePrimitiveArrayCritical(env, in, src, JNI_ABORT);
+    if (o) (*env)->ReleaseLongArrayElements(env, offs, o, JNI_ABORT);
+    if (rc != LZMA_OK) {
+        throw_io(env, rc == LZMA_E_NOMEM && !(o && src && dst) ? "could not pin the Java arrays" : lzma_mctx_last_error(g_m));
+        pthread_mutex_unlock(&g_lock);
+        free(oo);
+        return NULL;
+    }
+    pthread_mutex_unlock(&g_lock);
+    jlongArray r = (*env)->NewLongArray(env, n + 1);
+    if (r) (*env)->SetLongArrayRegion(env, r, 0, n + 1, (const jlong *)oo);
+    free(oo);
+    return r;
+}
