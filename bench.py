@@ -58,6 +58,13 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=128 << 20,
                     help="bytes of the workload the multi-thread CPU baseline encodes+decodes (0 = skip)")
     ap.add_argument("--cpu-single", type=int, default=8 << 20, help="bytes for the 1-thread CPU baseline")
+    ap.add_argument("--cpu-threads", default="share,node_share,nproc",
+                    help="thread counts the multi-thread CPU baseline is timed at: 'share' = the job's CPU quota "
+                         "(cgroup cpu.max, else OMP_NUM_THREADS / affinity), 'node_share' = nproc / 8 (one GPU's "
+                         "share of an 8-GPU node), 'nproc' = every visible CPU, or integers")
+    ap.add_argument("--single-stream", type=int, default=16 << 20,
+                    help="bytes of the one-stream measurement after the timed region (SURVEY 7.3's serial tail, "
+                         "config 4's regime): GPU encode/decode of one stream beside the oracle on 1 thread (0 = skip)")
     ap.add_argument("--parity-streams", type=int, default=16,
                     help="streams each rank checks against the oracle when there is no cpu_baseline sample")
     ap.add_argument("--no-verify", action="store_true")
@@ -237,6 +244,10 @@ def main():
         torch.distributed.all_reduce(flag[1:], op=torch.distributed.ReduceOp.SUM)
         ok, checked = bool(flag[0].item()), int(flag[1].item())
 
+    single = None
+    if rank == 0 and world == 1 and args.single_stream > 0:
+        single = single_stream(args, full, p, dev, st, orc if op is not None else None, op)
+
     total_bytes = (size if args.strong else size * world) * args.steps
     value = total_bytes / elapsed / 1e6
 
@@ -280,7 +291,7 @@ def main():
             "parity_streams_checked": checked, "roundtrip_ok": roundtrip,
             "gathered_bytes_rank0": state.get("gathered"),
             "kernels_ms": {k: {"total_ms": v[0], "launches": v[1]} for k, v in timings.items()},
-            "roofline": roofline, "cpu_baseline": cpu,
+            "roofline": roofline, "cpu_baseline": cpu, "single_stream": single,
         }
         print(json.dumps(res), flush=True)
     ctx.close()
@@ -387,20 +398,96 @@ def cpu_baseline(orc, op, chunks, args):
         return encs, {"value": nbytes / (t2 - t0) / 1e6, "compress_MBps": nbytes / (t1 - t0) / 1e6,
                       "decompress_MBps": nbytes / (t2 - t1) / 1e6, "bytes": nbytes, "streams": len(idx)}
 
-    threads = orc.cpu_threads()
+    nproc = os.cpu_count() or 1
+    quota = cgroup_cpus()
+    named = {"share": quota or orc.cpu_threads(), "node_share": max(1, nproc // 8), "nproc": nproc}
+    counts = []
+    for t in args.cpu_threads.split(","):
+        t = t.strip()
+        c = named[t] if t in named else int(t)
+        if c not in counts:
+            counts.append(c)
     one_idx = spread(n, max(1, args.cpu_single // chunk))
     _, one = run(one_idx, 1)
     multi_idx = spread(n, max(1, args.cpu_sample // chunk))
-    encs, multi = run(multi_idx, threads)
-    res = {"value": multi["value"], "unit": "MB/s", "cores": threads, "kind": "port",
+    by_threads, encs = {}, None
+    for c in counts:
+        e, r = run(multi_idx, c)
+        encs = encs or e
+        by_threads[str(c)] = r
+    best = max(by_threads, key=lambda k: by_threads[k]["value"])
+    multi = by_threads[best]
+    res = {"value": multi["value"], "unit": "MB/s", "cores": int(best), "kind": "port",
            "compress_MBps": multi["compress_MBps"], "decompress_MBps": multi["decompress_MBps"],
-           "cpu_model": cpu_model(), "cpus_visible": os.cpu_count(),
+           "cpu_model": cpu_model(), "cpus_visible": nproc, "cgroup_cpu_quota": quota,
+           "node_share_cpus": named["node_share"],
+           "by_threads": {k: {"value": v["value"], "compress_MBps": v["compress_MBps"],
+                              "decompress_MBps": v["decompress_MBps"]} for k, v in by_threads.items()},
            "single_thread": dict(one, cores=1),
            "sample": "%d of the %d streams (%d MiB, spread evenly over the buffer), oracle/ C restatement of the "
-                     "Java reference (no JDK on the box), one reused encoder per thread, %d threads; "
-                     "single_thread: %d streams on 1 thread" % (len(multi_idx), n, multi["bytes"] >> 20, threads,
-                                                                len(one_idx))}
+                     "Java reference (no JDK on the box), one reused encoder per thread, timed at %s threads "
+                     "(the job's cgroup CPU quota, nproc / 8 and nproc); value = the fastest (%s threads); "
+                     "single_thread: %d streams on 1 thread"
+                     % (len(multi_idx), n, multi["bytes"] >> 20, "/".join(str(c) for c in counts), best,
+                        len(one_idx))}
     return res, dict(zip(multi_idx, encs))
+
+
+def cgroup_cpus():
+    """CPUs the job may use per the cgroup quota (cpu.max 'quota period'), or None."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            return max(1, int(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def single_stream(args, full, p, dev, st, orc, op):
+    """SURVEY 7.3's serial tail (config 4's regime: one stream far longer than a chunk): one
+    stream of --single-stream bytes of the same data, dict as the workload, encoded and decoded
+    on the GPU (device-resident, one wave parses it: the solo kernel), beside the oracle on one
+    host thread on the same bytes; the GPU bytes must equal the oracle's."""
+    n = min(args.single_stream, full.size)
+    host = full[:n]
+    d_in = torch.from_numpy(host).to(dev)
+    cap = lzma_amd.enc_bound(n)
+    d_out = torch.empty(cap + 1, dtype=torch.uint8, device=dev)
+    d_dec = torch.empty(n + 1, dtype=torch.uint8, device=dev)
+    ctx = lzma_amd.Context(dev.index)
+    ctx.set_batch_bytes(max(n, 1 << 20))
+    ctx.set_timing(True)
+    offs = np.array([0, n], dtype=np.uint64)
+    coffs = np.array([0, cap], dtype=np.uint64)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    lens = ctx.encode_batch_dev(d_in, offs, p, d_out, coffs, st)
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    dl, ds = ctx.decode_batch_dev(lzma_amd.write_props(p), d_out, np.array([0, int(lens[0])], dtype=np.uint64),
+                                  np.array([n], dtype=np.int64), d_dec, offs, st)
+    torch.cuda.synchronize(dev)
+    t2 = time.perf_counter()
+    tm = ctx.timings()
+    ctx.close()
+    enc = d_out[:int(lens[0])].cpu().numpy().tobytes()
+    ok = int(ds[0]) == 0 and int(dl[0]) == n and bool(torch.equal(d_dec[:n], d_in))
+    res = {"bytes": int(n), "dict_log": int(p.dict_size).bit_length() - 1, "gpu_compress_MBps": n / (t1 - t0) / 1e6,
+           "gpu_decompress_MBps": n / (t2 - t1) / 1e6, "parse_ms": tm.get("enc_parse", (0.0, 0))[0],
+           "parse_cycles_per_byte": tm.get("enc_parse", (0.0, 0))[0] / 1e3 * 2.4e9 / max(n, 1),
+           "ratio": len(enc) / max(n, 1), "roundtrip_ok": ok}
+    if orc is not None:
+        data = host.tobytes()
+        c0 = time.perf_counter()
+        ref = orc.EncoderSession(op).encode(data)
+        c1 = time.perf_counter()
+        rc, back = orc.decode(ref, orc.props(op), n)
+        c2 = time.perf_counter()
+        res.update(cpu_1thread_compress_MBps=n / (c1 - c0) / 1e6, cpu_1thread_decompress_MBps=n / (c2 - c1) / 1e6,
+                   equals_oracle=ref == enc, gpu_over_cpu_compress=(c1 - c0) / (t1 - t0))
+    return res
 
 
 if __name__ == "__main__":

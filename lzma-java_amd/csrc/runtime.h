@@ -330,11 +330,14 @@ struct DecArgs {
     unsigned int* next;
     uint8_t* scratch;             // per-block literal probs when they do not fit LDS
     uint64_t scratch_stride;
-    uint32_t lc, lp, pb, dict_check, lit_in_lds;
+    uint32_t lc, lp, pb, dict_check;
+    uint32_t lit_lds_coders;      // literal coders 0 .. lit_lds_coders-1 live in LDS, the rest in `scratch`
 };
 
 int launch_decoder(Ctx* ctx, const DecArgs& a, int grid, hipStream_t st);
-int dec_grid(uint32_t lc, uint32_t lp, uint32_t lit_in_lds, int nstreams);
+int dec_grid(int nstreams);
+// literal coders of a stream the decoder keeps in LDS when `per_cu` streams share a CU
+uint32_t dec_lit_lds_coders(uint32_t lc, uint32_t lp, uint32_t pb, int per_cu);
 int enc_grid(const Derived& d, int nstreams);
 size_t enc_lds_bytes(const EncArgs& a);
 size_t dec_scratch_per_block(uint32_t lc, uint32_t lp);

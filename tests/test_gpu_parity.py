@@ -387,3 +387,20 @@ def test_gpu_single_stream_c_abi(ctx):
     small = (ctypes.c_uint8 * 1000)()
     rc = L.lzma_decode(ctx.h, props, enc, len(enc), -1, small, 1000, ctypes.byref(m))
     assert rc == lzma_amd.LZMA_E_OVERFLOW
+
+
+@pytest.mark.timeout(600)
+def test_gpu_config4_shape_one_stream_longer_than_dict(ctx, heartbeat):
+    """Config 4's regime: ONE BENCH stream far longer than a chunk and longer than its
+    dictionary (72 MiB at dict 2^26, L5), so the window expires for the last 8 MiB
+    (matchMinPos, BinTree.java:164, 231) and the pairs are the 64-bit form (> 8 MiB).
+    Encoder.Code (Encoder.java:1064-1077) on the whole stream: byte-equal to the oracle.
+    The parse is one wave's serial chain (the solo kernel), ~0.45 MB/s: minutes."""
+    n = 72 << 20
+    data = lzma_amd.bench_generate(n)
+    p = lzma_amd.make_params(dict_size=1 << 26, fb=32, mf=1, lc=3, lp=0, pb=2)
+    ctx.set_batch_bytes(1 << 30)
+    out = ctx.encode_batch([data], p)[0]
+    ref = orc.EncoderSession(_oparams(p)).encode(data.tobytes())
+    assert len(out) == len(ref)
+    assert out == ref

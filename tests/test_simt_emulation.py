@@ -27,3 +27,17 @@ def test_emulated_kernels_bit_exact_under_asan(parse_kernel):
     assert "0 failures" in r.stdout, tail
     errors = [l for l in r.stderr.splitlines() if "runtime error" in l and "emu_check.cpp" not in l]
     assert not errors, "\n".join(errors[:10])
+
+
+@pytest.mark.timeout(900)
+def test_emulated_range_coder_exact_replay_path_bit_exact():
+    """rc.hip's exact-replay path (taken by a block with a pending run of
+    0xFF bytes, about once per 2^16 shifts) built to run for EVERY block
+    (LZG_RC_FORCE_REPLAY), bit-exact against the oracle on the same inputs."""
+    subprocess.check_call(["make", "-s", "-j", "8", "-C", SIMT, "replay"])
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0", UBSAN_OPTIONS="print_stacktrace=1")
+    r = subprocess.run([os.path.join(SIMT, "build", "replay", "emu_check"), "quick"], capture_output=True, text=True,
+                       env=env, timeout=600)
+    tail = "\n".join((r.stdout + r.stderr).splitlines()[-20:])
+    assert r.returncode == 0, tail
+    assert "0 failures" in r.stdout, tail
