@@ -11,16 +11,12 @@
 //     of the lanes (readlane) and writes each adapted probability back as it
 //     goes (the nodes along one path are distinct, so the prefetched values
 //     stay exact for the rest of the walk);
-//   * the literal coders (0x300 << (lc + lp) probabilities): as many as fit
-//     the stream's share of the CU's LDS live in LDS (coders 0 .. K-1: with
-//     lc 3 lp 0, the contexts of a previous byte below 0x80, i.e. all of
-//     ASCII text), the rest in a per-stream HBM area; 16 streams share a CU
-//     at the bench's 4096 streams (fixed models, input ring, output window
-//     ~3.5 KiB + 4 coders of 1.5 KiB each); a literal's whole coder tree (plus
-//     the 8 matched-mode nodes along the match byte) is fetched in one round
-//     trip, issued before the isMatch decision so it overlaps with it. An
-//     HBM-resident coder's model writes stay in L2 once fewer coders live
-//     there (512 streams x 6 KiB per XCD fit its 4 MB L2; all 8 coders did not);
+//   * the literal coders (0x300 << (lc + lp) probabilities) live in a
+//     per-stream HBM area, so the LDS per stream stays small (fixed models,
+//     input ring, output window: ~3.5 KiB) and 16 streams share a CU; a
+//     literal's whole coder tree (plus the 8 matched-mode nodes along the
+//     match byte) is fetched in one round trip, issued before the isMatch
+//     decision so it overlaps with it;
 //   * compressed input is staged through an LDS ring (kIbuf bytes, refilled
 //     by all lanes at once);
 //   * the most recent kWin output bytes live in an LDS window (OutWindow,
@@ -62,9 +58,7 @@ struct Dec {
     using PL = ProbLayout<PBS>;
     uint32_t lane;
     uint16_t* probs;              // LDS: fixed models
-    uint16_t* lit;                // HBM: literal coders of this stream (those >= lit_k)
-    uint16_t* lit_l;              // LDS: literal coders 0 .. lit_k-1
-    uint32_t lit_k;
+    uint16_t* lit;                // HBM: literal coders of this stream
     uint8_t* ibuf;                // LDS [kIbuf]
     uint8_t* win;                 // LDS [kWin]
     uint32_t lc, lp, pb, ps_mask, dict_check;
@@ -280,10 +274,7 @@ struct Dec {
         const uint32_t nlit = 0x300u << (lc + lp);
         for (uint32_t i0 = 0; i0 < (uint32_t)PL::COUNT; i0 += kWave)
             if (i0 + lane < (uint32_t)PL::COUNT) probs[i0 + lane] = kBitModelTotal >> 1;
-        const uint32_t nl = 0x300u * lit_k;   // LDS part
-        for (uint32_t i0 = 0; i0 < nl; i0 += 2 * kWave)   // u32 pairs (0x300 is even)
-            if (i0 + 2 * lane < nl) *(uint32_t*)(lit_l + i0 + 2 * lane) = (kBitModelTotal >> 1) * 0x10001u;
-        for (uint32_t i0 = nl; i0 < nlit; i0 += 2 * kWave)
+        for (uint32_t i0 = 0; i0 < nlit; i0 += 2 * kWave)   // u32 pairs (nlit is even)
             if (i0 + 2 * lane < nlit) *(uint32_t*)(lit + i0 + 2 * lane) = (kBitModelTotal >> 1) * 0x10001u;
         LANE_FENCE();
         ipos = 0;
@@ -309,9 +300,7 @@ struct Dec {
             // (nodes 0-255) and, in matched mode, the 8 nodes along the match byte
             const bool matched = !st_is_char(state);   // only right after a match / rep: copy() left mb
             const uint32_t mb = matched ? mb_next : 0u;
-            const uint32_t cidx = ((now & ((1u << lp) - 1)) << lc) + (prev >> (8 - lc));
-            // a generic pointer: LDS for the first lit_k coders, HBM for the rest (flat loads/stores)
-            uint16_t* sub = (cidx < lit_k ? lit_l : lit) + (size_t)cidx * 0x300;
+            uint16_t* sub = lit + (size_t)(((now & ((1u << lp) - 1)) << lc) + (prev >> (8 - lc))) * 0x300;
             T256 tt;
             uint32_t mv[kVS];
             fetch256(sub, tt);
@@ -435,8 +424,6 @@ __global__ void __launch_bounds__(kWave) dec_kernel(DecArgs a) {
     d.probs = (uint16_t*)take((size_t)ProbLayout<PBS>::COUNT * 2);
     d.ibuf = take(kIbuf);
     d.win = take(kWin);
-    d.lit_k = a.lit_lds_coders;
-    d.lit_l = (uint16_t*)take((size_t)a.lit_lds_coders * 0x300 * 2);
     d.lit = (uint16_t*)(a.scratch + (size_t)blockIdx.x * a.scratch_stride);
     // one workgroup per stream; per-stream values are wave-uniform (readfirstlane keeps them scalar)
     const int s = __builtin_amdgcn_readfirstlane((int)a.order[blockIdx.x]);
@@ -456,34 +443,21 @@ __global__ void __launch_bounds__(kWave) dec_kernel(DecArgs a) {
 // literal coders of one stream (HBM), 256-byte aligned
 size_t dec_scratch_per_block(uint32_t lc, uint32_t lp) { return ((size_t)0x300 << (lc + lp)) * 2 + 256; }
 
-static size_t dec_lds_bytes(uint32_t pb, uint32_t lit_coders) {
+static size_t dec_lds_bytes(uint32_t pb) {
     auto r = [](size_t b) { return (b + 15) & ~(size_t)15; };
-    return r((size_t)prob_count(pb) * 2) + r(kIbuf) + r(kWin) + r((size_t)lit_coders * 0x300 * 2);
+    return r((size_t)prob_count(pb) * 2) + r(kIbuf) + r(kWin);
 }
 
-int dec_grid(int nstreams) { return nstreams; }   // one workgroup per stream
-
-// As many literal coders in LDS as the stream's share of the CU's 160 KiB allows, up to all
-// of them; at the bench's 16 streams per CU that is 4 of lc 3's 8 coders.
-uint32_t dec_lit_lds_coders(uint32_t lc, uint32_t lp, uint32_t pb, int per_cu) {
-    const size_t share = (160u * 1024u) / (size_t)(per_cu < 1 ? 1 : per_cu);
-    const size_t fixed = dec_lds_bytes(pb, 0);
-    const uint32_t all = 1u << (lc + lp);
-    if (share <= fixed) return 0;
-    const size_t k = (share - fixed) / (0x300 * 2);
-    return k >= all ? all : (uint32_t)k;
-}
+int dec_grid(uint32_t, uint32_t, uint32_t, int nstreams) { return nstreams; }   // one workgroup per stream
 
 template <int PBS>
 static void launch_dec(const DecArgs& a, int grid, size_t lds, hipStream_t st) {
-    if (lds > 64 * 1024) hipFuncSetAttribute((const void*)dec_kernel<PBS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL((dec_kernel<PBS>), dim3(grid), dim3(kWave), lds, st, a);
 }
 
 int launch_decoder(Ctx* ctx, const DecArgs& a, int grid, hipStream_t st) {
-    if (a.scratch == nullptr) return ctx->fail(LZMA_E_INTERNAL, "decoder needs the literal-coder scratch");
-    const size_t lds = dec_lds_bytes(a.pb, a.lit_lds_coders);
-    if (lds > 160 * 1024) return ctx->fail(LZMA_E_INTERNAL, "decoder LDS %zu too large", lds);
+    if (a.lit_in_lds || a.scratch == nullptr) return ctx->fail(LZMA_E_INTERNAL, "decoder needs the literal-coder scratch");
+    const size_t lds = dec_lds_bytes(a.pb);
     TimedLaunch tl(ctx, "dec_stream", st);
     if (a.pb <= 2) launch_dec<2>(a, grid, lds, st); else launch_dec<4>(a, grid, lds, st);
     hipError_t e = hipGetLastError();

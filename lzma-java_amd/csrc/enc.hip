@@ -37,8 +37,7 @@ static __constant__ Tables c_tab = make_tables();
 
 constexpr int kOptLds = 64;         // _optimum slots kept in LDS (deeper slots spill to HBM); the LDS arrays
                                     // have one more slot, kOptLds, a sink for the writes of idle lanes
-constexpr int kLitLdsMaxBits = 1;   // batch kernel: literal coders in LDS when lc + lp <= 1 (<= 3 KiB); else HBM/L2
-constexpr int kLitLdsMaxBitsSolo = 4;   // solo kernel (<= 4 streams per CU): up to 24 KiB in LDS
+constexpr int kLitLdsMaxBits = 1;   // literal coders in LDS when lc + lp <= 1 (<= 3 KiB); else HBM/L2
 constexpr int kMdCap = kMatchMaxLen + 1;
 constexpr int kRing = 32;           // match-info prefetch window (positions)
 constexpr int kGW = 64;             // gather window: offsets -1 .. kGW-2 around the current position
@@ -46,6 +45,7 @@ constexpr int kGI = kGW / kWave;    // gather iterations per side (1 on hardware
 constexpr int kSides = 7;           // cur, rep0..rep3, pair0, pair1
 constexpr int kRbuf = 128;          // coder-record staging ring (records, power of two; halves of 64 go to HBM)
 constexpr int kLitSlots = (8 + kWave - 1) / kWave;   // literal bits per lane (1 on hardware)
+static_assert(kSides * kGW >= kNumFullDistances * 2, "tempPrices alias the gather window");
 
 #define FI __device__ __forceinline__
 // Lanes of one wavefront exchange data through LDS. The hardware runs one
@@ -81,40 +81,6 @@ constexpr int kLitSlots = (8 + kWave - 1) / kWave;   // literal bits per lane (1
 #define PEND(k, v) do {} while (0)
 #define PCOUNT(k) do {} while (0)
 #endif
-
-// Slot vectors: the first kOptLds _optimum slots of one field live in VGPRs,
-// slot s in lane s % kWave of register s / kWave (one register on hardware). A
-// uniform slot read is one v_readlane and a write one v_writelane (no LDS round
-// trip on getOptimum's serial chain); the per-length relax loops give lane j
-// the slot j, so a candidate compares and updates its slot in registers.
-constexpr int kSV = (kOptLds + kWave - 1) / kWave;
-struct SV {
-    uint32_t r[kSV];
-};
-FI uint32_t sv_get(const SV& v, uint32_t s) {   // s < kOptLds, wave-uniform
-    if constexpr (kSV == 1) return (uint32_t)__builtin_amdgcn_readlane((int)v.r[0], (int)s);
-    uint32_t x = 0;
-#pragma unroll
-    for (int k = 0; k < kSV; k++)
-        if ((uint32_t)k == s / kWave) x = (uint32_t)__builtin_amdgcn_readlane((int)v.r[k], (int)(s % kWave));
-    return x;
-}
-FI void sv_set(SV& v, uint32_t s, uint32_t x) {   // s < kOptLds, x wave-uniform
-#pragma unroll
-    for (int k = 0; k < kSV; k++)
-        if (kSV == 1 || (uint32_t)k == s / kWave)
-            v.r[k] = (uint32_t)lzg_writelane((int)x, (int)(s % kWave), (int)v.r[k]);
-}
-
-// A value the optimiser cannot see through. A select between two struct members
-// would otherwise become a load through a selected address, which keeps the whole
-// per-stream state struct in scratch memory instead of registers.
-FI uint32_t opaque(uint32_t x) {
-#if LZG_WAVE == 64
-    asm volatile("" : "+v"(x));
-#endif
-    return x;
-}
 
 FI uint64_t uni64(uint64_t v) {
     return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32)) << 32) |
@@ -152,10 +118,7 @@ FI uint32_t sel4(uint32_t i, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
 // FairPrio rows of the encoder's waves (lzma_common.h)
 __device__ uint32_t g_enc_sched[kSchedRows * kSchedCols];
 
-// RS: the _optimum slots below kOptLds and the gather window live in registers
-// (the solo kernel: few streams, one wave per SIMD, latency first); otherwise in
-// LDS (the batch kernel: 16 waves per CU share 128 VGPRs each).
-template <typename PairT, bool LIT_LDS, int PBS, bool RS>
+template <typename PairT, bool LIT_LDS, int PBS>
 struct Enc {
     using PP = PairPack<PairT>;
     using PL = ProbLayout<PBS>;
@@ -180,24 +143,15 @@ struct Enc {
     uint32_t* md_dist;
     uint32_t* ring_info;      // [kRing]
     PairT* ring_pairs;        // [kRing * kInlinePairs]
-    // ---- _optimum slots < kOptLds: price, pos_prev | pos_prev2 << 16, back_prev, back_prev2, flags
-    // (prev1IsChar | prev2 << 1 | state << 4), the 4 reps, and the bytes (cur | match << 8 | previous
-    // << 16) of each parsed position, so the coder needs no HBM byte loads.
-    // RS: registers (SV)
-    SV r_price, r_pp, r_bp, r_bp2, r_fs, r_bytes;
-    SV r_backs[4];
-    // !RS: LDS SoA, [kOptLds + 1] each (slot kOptLds is a sink for the writes of idle lanes)
-    uint32_t* o_price;
+    uint32_t* o_price;        // _optimum SoA, [kOptLds] each
     uint32_t* o_pp;
     int32_t* o_bp;
     int32_t* o_bp2;
     uint8_t* o_fs;
     uint32_t* o_backs;        // [4][kOptLds]
-    uint32_t* o_bytes;
-    uint8_t* win;             // !RS: the gather window [kSides][kGW] in LDS (also tempPrices)
-    // ---- RS: the per-position gather window in registers: side 0 = cur, 1-4 = reps 0-3, 5-6 = pairs 0-1;
-    // offset o (-1 .. kGW-2) of a side is lane (o + 1) % kWave of g_win[side][(o + 1) / kWave]
-    uint32_t g_win[kSides][kGI];
+    uint32_t* o_bytes;        // [kOptLds] cur byte | match byte << 8 | previous byte << 16 of each parsed
+                              // position, so the coder needs no HBM byte loads
+    uint8_t* win;             // gather window [kSides][kGW]: cur side, reps 0-3, pairs 0-1
     uint16_t* rbuf;           // coder-record staging ring [kRbuf]
     __amdgpu_buffer_rsrc_t spill;   // _optimum slots >= kOptLds in HBM (9 fields x kNumOpts dwords)
     // ---- parameters
@@ -244,48 +198,27 @@ struct Enc {
     FI void sstore(uint32_t field, uint32_t i, uint32_t v) {
         __builtin_amdgcn_raw_buffer_store_b32(v, spill, (field * kNumOpts + i) * 4, 0, 0);
     }
-    // uniform slot accessors: registers (RS) or LDS below kOptLds (F: the caller knows i < kOptLds),
-    // HBM spill above
-#define SLOT_GET(R, L, FIELD, i) \
-    if (F || (i) < (uint32_t)kOptLds) { if constexpr (RS) return sv_get(R, i); else return (uint32_t)(L)[i]; } \
-    return sload(FIELD, i)
-#define SLOT_SET(R, L, T, FIELD, i, v) \
-    if (F || (i) < (uint32_t)kOptLds) { if constexpr (RS) sv_set(R, i, (uint32_t)(v)); else (L)[i] = (T)(v); } \
-    else sstore(FIELD, i, (uint32_t)(v))
-    template <bool F = false> FI uint32_t price_at(uint32_t i) const { SLOT_GET(r_price, o_price, 0, i); }
-    template <bool F = false> FI void set_price(uint32_t i, uint32_t v) { SLOT_SET(r_price, o_price, uint32_t, 0, i, v); }
-    template <bool F = false> FI uint32_t pp_at(uint32_t i) const { SLOT_GET(r_pp, o_pp, 1, i); }
-    template <bool F = false> FI void set_pp(uint32_t i, uint32_t v) { SLOT_SET(r_pp, o_pp, uint32_t, 1, i, v); }
-    template <bool F = false> FI int32_t bp_at(uint32_t i) const { return (int32_t)bpu_at<F>(i); }
-    template <bool F = false> FI uint32_t bpu_at(uint32_t i) const { SLOT_GET(r_bp, o_bp, 2, i); }
-    template <bool F = false> FI void set_bp(uint32_t i, int32_t v) { SLOT_SET(r_bp, o_bp, int32_t, 2, i, v); }
-    template <bool F = false> FI int32_t bp2_at(uint32_t i) const { return (int32_t)bp2u_at<F>(i); }
-    template <bool F = false> FI uint32_t bp2u_at(uint32_t i) const { SLOT_GET(r_bp2, o_bp2, 3, i); }
-    template <bool F = false> FI void set_bp2(uint32_t i, int32_t v) { SLOT_SET(r_bp2, o_bp2, int32_t, 3, i, v); }
-    template <bool F = false> FI uint32_t fs_at(uint32_t i) const { SLOT_GET(r_fs, o_fs, 4, i); }
-    template <bool F = false> FI void set_fs(uint32_t i, uint32_t v) { SLOT_SET(r_fs, o_fs, uint8_t, 4, i, v); }
-    template <bool F = false> FI uint32_t back_at(uint32_t i, int k) const { SLOT_GET(r_backs[k], o_backs + k * kOptLds, 5 + k, i); }
-    template <bool F = false> FI void set_back(uint32_t i, int k, uint32_t v) { SLOT_SET(r_backs[k], o_backs + k * kOptLds, uint32_t, 5 + k, i, v); }
-    template <bool F = false> FI uint32_t bytes_at(uint32_t i) const { SLOT_GET(r_bytes, o_bytes, 9, i); }
-    template <bool F = false> FI void set_bytes(uint32_t i, uint32_t v) { SLOT_SET(r_bytes, o_bytes, uint32_t, 9, i, v); }
-#undef SLOT_GET
-#undef SLOT_SET
-    // byte at offset o (-1 <= o <= kGW - 2) of a gathered side (see gather())
-    // (the side is picked by a select chain, never by a runtime register index, which would move
-    // g_win to scratch memory)
-    FI uint32_t gwin(int side, int32_t o) const {
-        const uint32_t k = (uint32_t)(o + 1);
-        const uint32_t it = kGI == 1 ? 0u : k / kWave;
-        uint32_t v = opaque(g_win[0][it]);
-#pragma unroll
-        for (int sd = 1; sd < kSides; sd++) v = side == sd ? opaque(g_win[sd][it]) : v;
-        return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)(k % kWave));
+    template <bool F = false> FI uint32_t price_at(uint32_t i) const { if (F || i < (uint32_t)kOptLds) return o_price[i]; return sload(0, i); }
+    template <bool F = false> FI void set_price(uint32_t i, uint32_t v) { if (F || i < (uint32_t)kOptLds) o_price[i] = v; else sstore(0, i, v); }
+    template <bool F = false> FI uint32_t pp_at(uint32_t i) const { if (F || i < (uint32_t)kOptLds) return o_pp[i]; return sload(1, i); }
+    template <bool F = false> FI void set_pp(uint32_t i, uint32_t v) { if (F || i < (uint32_t)kOptLds) o_pp[i] = v; else sstore(1, i, v); }
+    template <bool F = false> FI int32_t bp_at(uint32_t i) const { if (F || i < (uint32_t)kOptLds) return o_bp[i]; return (int32_t)sload(2, i); }
+    template <bool F = false> FI void set_bp(uint32_t i, int32_t v) { if (F || i < (uint32_t)kOptLds) o_bp[i] = v; else sstore(2, i, (uint32_t)v); }
+    template <bool F = false> FI int32_t bp2_at(uint32_t i) const { if (F || i < (uint32_t)kOptLds) return o_bp2[i]; return (int32_t)sload(3, i); }
+    template <bool F = false> FI void set_bp2(uint32_t i, int32_t v) { if (F || i < (uint32_t)kOptLds) o_bp2[i] = v; else sstore(3, i, (uint32_t)v); }
+    template <bool F = false> FI uint32_t fs_at(uint32_t i) const { if (F || i < (uint32_t)kOptLds) return (uint32_t)o_fs[i]; return sload(4, i); }
+    template <bool F = false> FI void set_fs(uint32_t i, uint32_t v) { if (F || i < (uint32_t)kOptLds) o_fs[i] = (uint8_t)v; else sstore(4, i, v); }
+    template <bool F = false> FI uint32_t back_at(uint32_t i, int k) const {
+        if (F || i < (uint32_t)kOptLds) return o_backs[k * kOptLds + i];
+        return sload(5 + k, i);
     }
-    // the gather window's bytes of the current position: cur | match (rep0 side) << 8 | previous << 16
-    FI uint32_t win_bytes() const {
-        if constexpr (RS) return gwin(0, 0) | (gwin(1, 0) << 8) | (gwin(0, -1) << 16);
-        return (uint32_t)win[1] | ((uint32_t)win[kGW + 1] << 8) | ((uint32_t)win[0] << 16);
+    template <bool F = false> FI void set_back(uint32_t i, int k, uint32_t v) {
+        if (F || i < (uint32_t)kOptLds) o_backs[k * kOptLds + i] = v; else sstore(5 + k, i, v);
     }
+    template <bool F = false> FI uint32_t bytes_at(uint32_t i) const { if (F || i < (uint32_t)kOptLds) return o_bytes[i]; return sload(9, i); }
+    template <bool F = false> FI void set_bytes(uint32_t i, uint32_t v) { if (F || i < (uint32_t)kOptLds) o_bytes[i] = v; else sstore(9, i, v); }
+    // the gather window's bytes of the current position (see gather())
+    FI uint32_t win_bytes() const { return (uint32_t)win[1] | ((uint32_t)win[kGW + 1] << 8) | ((uint32_t)win[0] << 16); }
     template <bool F = false> FI uint32_t pos_prev(uint32_t i) const { return pp_at<F>(i) & 0xFFFFu; }
     template <bool F = false> FI uint32_t pos_prev2(uint32_t i) const { return pp_at<F>(i) >> 16; }
     // after lanes wrote slots up to `hi`, make them visible to every lane
@@ -387,39 +320,13 @@ struct Enc {
     // o = -1 .. kGW-2 from p (the current byte) on the cur side and at
     // p + o - dist - 1 on the rep / match sides. gather() issues all of those
     // byte loads at once (one lane per offset, one memory round trip), keeps
-    // equality masks per side (bit o+1 = bytes equal at offset o) and keeps the
-    // bytes in registers (g_win) for the literal-price lookups, which read them
-    // with v_readlane at a uniform offset. Compares past the window fall back to
-    // match_len.
+    // equality masks per side (bit o+1 = bytes equal at offset o) and stores
+    // the bytes in the LDS window for the literal-price lookups. Compares past
+    // the window fall back to match_len.
     FI void gather(bool with_pairs) {
         gp = mfpos - 1;
         const uint32_t d0 = rp0 + 1, d1 = rp1 + 1, d2 = rp2 + 1, d3 = rp3 + 1;
         const uint32_t e0 = num_pairs > 0 ? md_dist[0] + 1 : d0, e1 = num_pairs > 1 ? md_dist[1] + 1 : d0;
-        if constexpr (RS) {
-#pragma unroll
-            for (int it = 0; it < kGI; it++) {
-                const uint32_t q = gp - 1 + (uint32_t)(it * kWave) + lane;
-                g_win[0][it] = in_byte(q);
-                g_win[1][it] = in_byte(q - d0); g_win[2][it] = in_byte(q - d1);
-                g_win[3][it] = in_byte(q - d2); g_win[4][it] = in_byte(q - d3);
-                if (with_pairs) { g_win[5][it] = in_byte(q - e0); g_win[6][it] = in_byte(q - e1); }
-            }
-            gm0 = gm1 = gm2 = gm3 = gmp0 = gmp1 = 0;
-#pragma unroll
-            for (int it = 0; it < kGI; it++) {
-                const int sh = it * kWave;
-                const uint32_t va = g_win[0][it];
-                gm0 |= (uint64_t)__ballot(va == g_win[1][it]) << sh;
-                gm1 |= (uint64_t)__ballot(va == g_win[2][it]) << sh;
-                gm2 |= (uint64_t)__ballot(va == g_win[3][it]) << sh;
-                gm3 |= (uint64_t)__ballot(va == g_win[4][it]) << sh;
-                if (with_pairs) {
-                    gmp0 |= (uint64_t)__ballot(va == g_win[5][it]) << sh;
-                    gmp1 |= (uint64_t)__ballot(va == g_win[6][it]) << sh;
-                }
-            }
-            return;
-        }
         uint32_t va[kGI], v0[kGI], v1[kGI], v2[kGI], v3[kGI], w0[kGI], w1[kGI];
 #pragma unroll
         for (int it = 0; it < kGI; it++) {
@@ -450,15 +357,12 @@ struct Enc {
     }
     // byte at p + o on the cur side
     FI uint32_t a_byte(int32_t o) const {
-        if (o >= -1 && o <= kGW - 2) { if constexpr (RS) return gwin(0, o); else return (uint32_t)win[o + 1]; }
-        return in_byte(gp + (uint32_t)o);
+        return (o >= -1 && o <= kGW - 2) ? (uint32_t)win[o + 1] : in_byte(gp + (uint32_t)o);
     }
     // byte at p + o - dist - 1 (side 1..6 = rep0..3, pair0..1; side < 0: not gathered)
     FI uint32_t b_byte(int side, uint32_t dist, int32_t o) const {
-        if (side > 0 && o >= -1 && o <= kGW - 2) {
-            if constexpr (RS) return gwin(side, o); else return (uint32_t)win[side * kGW + o + 1];
-        }
-        return in_byte(gp + (uint32_t)o - dist - 1);
+        return (side > 0 && o >= -1 && o <= kGW - 2) ? (uint32_t)win[side * kGW + o + 1]
+                                                       : in_byte(gp + (uint32_t)o - dist - 1);
     }
     // InWindow.GetMatchLen(index = o - 1, dist, limit) from the side's mask; the
     // part of the compare beyond the window continues with match_len.
@@ -761,39 +665,24 @@ struct Enc {
     FI uint32_t pos_len_price(uint32_t pos, uint32_t len, uint32_t ps) const {   // Encoder.java:323-333
         return dist_price(pos, len) + len_price(0, len - kMatchMinLen, ps);
     }
-    // _optimum[a + 1 .. b].Price = kIfinityPrice: register slots by lane, spill slots by LANE_FOR
-    FI void fill_inf(uint32_t a, uint32_t b) {
-        if constexpr (!RS) {
-            if (b < (uint32_t)kOptLds) {   // branch-free: idle lanes write the sink slot
-                for (uint32_t i0 = a + 1; i0 <= b; i0 += kWave) {
-                    const uint32_t i = i0 + lane;
-                    o_price[i <= b ? i : (uint32_t)kOptLds] = kInfinityPrice;
-                }
-                LANE_FENCE();
-                return;
-            }
-            LANE_FOR(uint32_t, i, a + 1, b + 1) set_price(i, kInfinityPrice);
-            fence_upto(b);
-            return;
-        }
-#pragma unroll
-        for (int k = 0; k < kSV; k++) {
-            const uint32_t j = (uint32_t)(k * kWave) + lane;
-            r_price.r[k] = (j > a && j <= b) ? kInfinityPrice : r_price.r[k];
-        }
-        if (b >= (uint32_t)kOptLds) {
-            LANE_FOR(uint32_t, i, a + 1 > (uint32_t)kOptLds ? a + 1 : (uint32_t)kOptLds, b + 1) sstore(0, i, kInfinityPrice);
-            SPILL_FENCE();
-        }
-    }
     // while (lenEnd < target) _optimum[++lenEnd].Price = kIfinityPrice
     FI void extend_to(uint32_t& len_end, uint32_t target) {
         if (len_end >= target) return;
-        fill_inf(len_end, target);
+        if (target < (uint32_t)kOptLds) {   // branch-free: idle lanes write the sink slot
+            for (uint32_t i0 = len_end + 1; i0 <= target; i0 += kWave) {
+                const uint32_t i = i0 + lane;
+                o_price[i <= target ? i : (uint32_t)kOptLds] = kInfinityPrice;
+            }
+            len_end = target;
+            LANE_FENCE();
+            return;
+        }
+        LANE_FOR(uint32_t, i, len_end + 1, target + 1) set_price(i, kInfinityPrice);
         len_end = target;
+        fence_upto(target);
     }
-    // ---- !RS (LDS slots): lanes relax slots base+l, l in [lo, hi]
-    FI void relax_rep_l(uint32_t base_slot, uint32_t lo, uint32_t hi, uint32_t price_base, uint32_t ps,
+    // lanes relax slots base+l, l in [lo, hi], with a rep of index ri
+    FI void relax_rep(uint32_t base_slot, uint32_t lo, uint32_t hi, uint32_t price_base, uint32_t ps,
                       uint32_t pos_prev_v, uint32_t ri) {
         if (base_slot + hi < (uint32_t)kOptLds) {   // all slots in LDS: no per-lane spill branches
             // branch-free: idle lanes and lanes that do not improve write the sink slot
@@ -825,7 +714,7 @@ struct Enc {
         fence_upto(base_slot + hi);
     }
     // lanes relax slots base+l, l in [lo, hi], all with the match distance `dist`
-    FI void relax_match_l(uint32_t base_slot, uint32_t lo, uint32_t hi, uint32_t price_base, uint32_t dist, uint32_t ps,
+    FI void relax_match(uint32_t base_slot, uint32_t lo, uint32_t hi, uint32_t price_base, uint32_t dist, uint32_t ps,
                         uint32_t pos_prev_v) {
         if (base_slot + hi < (uint32_t)kOptLds) {   // all slots in LDS; branch-free as relax_rep
             for (uint32_t l0 = lo; l0 <= hi; l0 += kWave) {
@@ -857,7 +746,7 @@ struct Enc {
     }
     // getOptimum's match candidates of position 0 (Encoder.java:620-640)
     template <bool F>
-    FI void relax_first_l(uint32_t lstart, uint32_t len_main, uint32_t npairs, uint32_t normal_match_price, uint32_t pos_state) {
+    FI void relax_first(uint32_t lstart, uint32_t len_main, uint32_t npairs, uint32_t normal_match_price, uint32_t pos_state) {
         if (F) {   // all slots in LDS: branch-free (idle and non-improving lanes write the sink slot)
             for (uint32_t l0 = lstart; l0 <= len_main; l0 += kWave) {
                 const uint32_t l = l0 + lane;
@@ -893,114 +782,6 @@ struct Enc {
         }
         if (F) LANE_FENCE(); else fence_upto(len_main);
     }
-    // Relax slots base+l, l in [lo, hi]: in registers, lane j takes slot j (length j - base); the
-    // spill slots (>= kOptLds) one length per lane. Each length owns one slot, so the order of the
-    // candidates within a call does not matter; strict < keeps the first candidate on ties.
-    // rep of index ri (Encoder.java:704-716, 727-742)
-    FI void relax_rep(uint32_t base_slot, uint32_t lo, uint32_t hi, uint32_t price_base, uint32_t ps,
-                      uint32_t pos_prev_v, uint32_t ri) {
-        if constexpr (!RS) { relax_rep_l(base_slot, lo, hi, price_base, ps, pos_prev_v, ri); return; }
-        if (base_slot + lo < (uint32_t)kOptLds) {
-#pragma unroll
-            for (int k = 0; k < kSV; k++) {
-                const uint32_t j = (uint32_t)(k * kWave) + lane;
-                const bool ok = j >= base_slot + lo && j <= base_slot + hi;
-                const uint32_t cl = price_base + len_price(1, ok ? j - base_slot - 2 : 0u, ps);
-                const bool upd = ok && cl < r_price.r[k];
-                r_price.r[k] = upd ? cl : r_price.r[k];
-                r_pp.r[k] = upd ? (r_pp.r[k] & 0xFFFF0000u) | pos_prev_v : r_pp.r[k];
-                r_bp.r[k] = upd ? ri : r_bp.r[k];
-                r_fs.r[k] = upd ? r_fs.r[k] & ~1u : r_fs.r[k];
-            }
-        }
-        if (base_slot + hi >= (uint32_t)kOptLds) {
-            const uint32_t l0 = base_slot + lo >= (uint32_t)kOptLds ? lo : (uint32_t)kOptLds - base_slot;
-            LANE_FOR(uint32_t, l, l0, hi + 1) {
-                const uint32_t cl = price_base + len_price(1, l - 2, ps);
-                const uint32_t s = base_slot + l;
-                if (cl < sload(0, s)) {
-                    sstore(0, s, cl);
-                    sstore(1, s, (sload(1, s) & 0xFFFF0000u) | pos_prev_v);
-                    sstore(2, s, ri);
-                    sstore(4, s, sload(4, s) & ~1u);
-                }
-            }
-            SPILL_FENCE();
-        }
-    }
-    // match of distance `dist` (Encoder.java:760-790)
-    FI void relax_match(uint32_t base_slot, uint32_t lo, uint32_t hi, uint32_t price_base, uint32_t dist, uint32_t ps,
-                        uint32_t pos_prev_v) {
-        if constexpr (!RS) { relax_match_l(base_slot, lo, hi, price_base, dist, ps, pos_prev_v); return; }
-        if (base_slot + lo < (uint32_t)kOptLds) {
-#pragma unroll
-            for (int k = 0; k < kSV; k++) {
-                const uint32_t j = (uint32_t)(k * kWave) + lane;
-                const bool ok = j >= base_slot + lo && j <= base_slot + hi;
-                const uint32_t cl = price_base + pos_len_price(dist, ok ? j - base_slot : (uint32_t)kMatchMinLen, ps);
-                const bool upd = ok && cl < r_price.r[k];
-                r_price.r[k] = upd ? cl : r_price.r[k];
-                r_pp.r[k] = upd ? (r_pp.r[k] & 0xFFFF0000u) | pos_prev_v : r_pp.r[k];
-                r_bp.r[k] = upd ? dist + kNumRepDistances : r_bp.r[k];
-                r_fs.r[k] = upd ? r_fs.r[k] & ~1u : r_fs.r[k];
-            }
-        }
-        if (base_slot + hi >= (uint32_t)kOptLds) {
-            const uint32_t l0 = base_slot + lo >= (uint32_t)kOptLds ? lo : (uint32_t)kOptLds - base_slot;
-            LANE_FOR(uint32_t, l, l0, hi + 1) {
-                const uint32_t cl = price_base + pos_len_price(dist, l, ps);
-                const uint32_t s = base_slot + l;
-                if (cl < sload(0, s)) {
-                    sstore(0, s, cl);
-                    sstore(1, s, (sload(1, s) & 0xFFFF0000u) | pos_prev_v);
-                    sstore(2, s, dist + kNumRepDistances);
-                    sstore(4, s, sload(4, s) & ~1u);
-                }
-            }
-            SPILL_FENCE();
-        }
-    }
-    // getOptimum's match candidates of position 0 (Encoder.java:620-640): slot = length
-    FI void relax_first(uint32_t lstart, uint32_t len_main, uint32_t npairs, uint32_t normal_match_price, uint32_t pos_state) {
-        if constexpr (!RS) {
-            if (len_main < (uint32_t)kOptLds) relax_first_l<true>(lstart, len_main, npairs, normal_match_price, pos_state);
-            else relax_first_l<false>(lstart, len_main, npairs, normal_match_price, pos_state);
-            return;
-        }
-        if (lstart < (uint32_t)kOptLds) {
-#pragma unroll
-            for (int k = 0; k < kSV; k++) {
-                const uint32_t l = (uint32_t)(k * kWave) + lane;
-                const bool ok = l >= lstart && l <= len_main;
-                // the pair of length l: the first with md_len >= l (lengths increase), i.e. the count of
-                // shorter ones among the first npairs - 1 -- a uniform loop instead of a per-lane while
-                uint32_t kp = 0;
-                for (uint32_t kk = 0; kk + 1 < npairs; kk++) kp += l > md_len[kk] ? 1u : 0u;
-                const uint32_t distance = md_dist[kp];
-                const uint32_t cl = normal_match_price + pos_len_price(distance, ok ? l : (uint32_t)kMatchMinLen, pos_state);
-                const bool upd = ok && cl < r_price.r[k];
-                r_price.r[k] = upd ? cl : r_price.r[k];
-                r_pp.r[k] = upd ? r_pp.r[k] & 0xFFFF0000u : r_pp.r[k];
-                r_bp.r[k] = upd ? distance + kNumRepDistances : r_bp.r[k];
-                r_fs.r[k] = upd ? r_fs.r[k] & ~1u : r_fs.r[k];
-            }
-        }
-        if (len_main >= (uint32_t)kOptLds) {
-            LANE_FOR(uint32_t, l, lstart > (uint32_t)kOptLds ? lstart : (uint32_t)kOptLds, len_main + 1) {
-                uint32_t kp = 0;
-                while (kp + 1 < npairs && l > md_len[kp]) kp++;
-                const uint32_t distance = md_dist[kp];
-                const uint32_t cl = normal_match_price + pos_len_price(distance, l, pos_state);
-                if (cl < sload(0, l)) {
-                    sstore(0, l, cl);
-                    sstore(1, l, sload(1, l) & 0xFFFF0000u);
-                    sstore(2, l, distance + kNumRepDistances);
-                    sstore(4, l, sload(4, l) & ~1u);
-                }
-            }
-            SPILL_FENCE();
-        }
-    }
     // uniform single-slot update for the two-step (x + literal + rep0) candidates
     template <bool F> FI void relax_two_step_t(uint32_t s, uint32_t cl, uint32_t pos_prev_v, bool prev2, uint32_t pos_prev2_v, int32_t back2) {
         if (cl < price_at<F>(s)) {
@@ -1015,7 +796,7 @@ struct Enc {
                 set_fs<F>(s, (fs_at<F>(s) & ~3u) | 1u);
             }
         }
-        if (!RS || !F) fence_upto(s);
+        fence_upto(s);
     }
 
     FI void relax_two_step(uint32_t s, uint32_t cl, uint32_t pos_prev_v, bool prev2, uint32_t pos_prev2_v, int32_t back2) {
@@ -1132,7 +913,13 @@ struct Enc {
         set_back<true>(0, 0, rp0); set_back<true>(0, 1, rp1); set_back<true>(0, 2, rp2); set_back<true>(0, 3, rp3);
         LANE_FENCE();
         PBEGIN(t2);
-        fill_inf(1, len_end);
+        if (len_end < (uint32_t)kOptLds) {
+            LANE_FOR(uint32_t, l, 2u, len_end + 1) set_price<true>(l, kInfinityPrice);
+            LANE_FENCE();
+        } else {
+            LANE_FOR(uint32_t, l, 2u, len_end + 1) set_price(l, kInfinityPrice);
+            fence_upto(len_end);
+        }
 #pragma unroll
         for (uint32_t i = 0; i < (uint32_t)kNumRepDistances; i++) {
             uint32_t rl = sel4(i, rl0, rl1, rl2, rl3);
@@ -1143,7 +930,8 @@ struct Enc {
         uint32_t lstart = rl0 >= 2 ? rl0 + 1 : 2;
         if (lstart <= len_main) {
             // no look-ahead in this loop: every length is independent
-            relax_first(lstart, len_main, npairs, normal_match_price, pos_state);
+            if (len_main < (uint32_t)kOptLds) relax_first<true>(lstart, len_main, npairs, normal_match_price, pos_state);
+            else relax_first<false>(lstart, len_main, npairs, normal_match_price, pos_state);
         }
         PEND(PF_RELAX, t2);
         return parse_forward(position, back_res, len_end);
@@ -1534,21 +1322,14 @@ struct Enc {
 
 // LDS layout of one stream's workgroup; shared by the kernel (carving) and
 // the host (dynamic LDS size). Regions are 16-byte aligned.
-// The _optimum regions (L_OPRICE .. L_OBYTES) and the gather window exist only in the
-// batch kernel's layout (a.solo == 0); the solo kernel keeps them in registers, and
-// L_WIN then only holds tempPrices.
-enum { L_PP, L_PROBS, L_DMP, L_LENP, L_LENC, L_PSP, L_DP, L_AP, L_MDLEN, L_MDDIST, L_RINFO, L_RPAIRS, L_OPRICE,
+enum { L_PP, L_PROBS, L_DMP, L_LENP, L_LENC, L_PSP, L_DP, L_AP, L_TP, L_MDLEN, L_MDDIST, L_RINFO, L_RPAIRS, L_OPRICE,
        L_OPP, L_OBP, L_OBP2, L_OFS, L_OBACKS, L_OBYTES, L_WIN, L_RBUF, L_LIT, L_COUNT };
-static_assert(kSides * kGW >= kNumFullDistances * 2, "tempPrices alias the gather window");
 __host__ __device__ inline uint32_t enc_lds_layout(const EncArgs& a, uint32_t* off) {
     const uint32_t md_cap = a.fb + 2;   // pairs per position <= fb (+1 clamp slot)
-    const uint32_t lds_slots = a.solo ? 0u : 1u;
     const uint32_t sz[L_COUNT] = {
         512 * 2, prob_count(a.pb) * 2 + 2, dm_count(a.pb) * 4 + 4, 2 * (1u << a.pb) * a.len_table_size * 2, 2 * 16 * 4, 256 * 2, 512 * 2, 16 * 4,
-        md_cap * 2, md_cap * 4, kRing * 4, kRing * kInlinePairs * a.pair_bytes,
-        lds_slots * (kOptLds + 1) * 4, lds_slots * (kOptLds + 1) * 4, lds_slots * (kOptLds + 1) * 4, lds_slots * kOptLds * 4,
-        lds_slots * (kOptLds + 1), lds_slots * 4 * kOptLds * 4, lds_slots * kOptLds * 4,
-        a.solo ? (uint32_t)kNumFullDistances * 2 : (uint32_t)(kSides * kGW), kRbuf * 2 + 2,
+        0u /* tp aliases the gather window */, md_cap * 2, md_cap * 4, kRing * 4, kRing * kInlinePairs * a.pair_bytes,
+        (kOptLds + 1) * 4, (kOptLds + 1) * 4, (kOptLds + 1) * 4, kOptLds * 4, kOptLds + 1, 4 * kOptLds * 4, kOptLds * 4, kSides * kGW, kRbuf * 2 + 2,
         a.lit_in_lds ? (0x300u << (a.lc + a.lp)) * 2 + 2 : 0u};
     uint32_t o = 0;
     for (int i = 0; i < L_COUNT; i++) { if (off) off[i] = o; o += (sz[i] + 15) & ~15u; }
@@ -1557,11 +1338,10 @@ __host__ __device__ inline uint32_t enc_lds_layout(const EncArgs& a, uint32_t* o
 
 // SPEC = 1: the level-5 parameters of bench.py (fb 32, lc 3, lp 0, pb 2, no end
 // marker) as compile-time constants; SPEC = 0: any parameters.
-// SOLO: the solo kernel's body (register slots, see Enc::RS).
-template <typename PairT, bool LIT_LDS, int PBS, int SPEC, bool SOLO>
-__device__ __forceinline__ void enc_body(const EncArgs& a) {
+template <typename PairT, bool LIT_LDS, int PBS, int SPEC>
+__global__ void __launch_bounds__(kWave, 4) enc_kernel(EncArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    Enc<PairT, LIT_LDS, PBS, SOLO> e;
+    Enc<PairT, LIT_LDS, PBS> e;
     e.lane = threadIdx.x;
     if (SPEC == 1) {
         e.fb = 32; e.lc = 3; e.lp = 0; e.pb = 2; e.ps_mask = 3; e.eos = 0; e.tsize = 31;
@@ -1573,10 +1353,7 @@ __device__ __forceinline__ void enc_body(const EncArgs& a) {
     uint32_t off[L_COUNT];
     {
         EncArgs la = a;   // SPEC: the layout folds to constants (immediate LDS offsets, no SGPR per region)
-        if (SPEC == 1) {
-            la.fb = 32; la.pb = 2; la.lc = 3; la.lp = 0; la.lit_in_lds = LIT_LDS ? 1 : 0;
-            la.pair_bytes = (uint32_t)sizeof(PairT); la.len_table_size = 31; la.solo = SOLO ? 1 : 0;
-        }
+        if (SPEC == 1) { la.fb = 32; la.pb = 2; la.lc = 3; la.lp = 0; la.lit_in_lds = 0; la.pair_bytes = 4; la.len_table_size = 31; }
         enc_lds_layout(la, off);
     }
     e.pp = (uint16_t*)(smem + off[L_PP]);
@@ -1586,6 +1363,7 @@ __device__ __forceinline__ void enc_body(const EncArgs& a) {
     e.psp = (uint16_t*)(smem + off[L_PSP]);
     e.dp = (uint16_t*)(smem + off[L_DP]);
     e.ap = (uint32_t*)(smem + off[L_AP]);
+    e.tp = (uint16_t*)(smem + off[L_WIN]);   // tempPrices only live inside fill_distances_prices
     e.dmp = (uint32_t*)(smem + off[L_DMP]);
     e.md_len = (uint16_t*)(smem + off[L_MDLEN]);
     e.md_dist = (uint32_t*)(smem + off[L_MDDIST]);
@@ -1599,18 +1377,6 @@ __device__ __forceinline__ void enc_body(const EncArgs& a) {
     e.o_backs = (uint32_t*)(smem + off[L_OBACKS]);
     e.o_bytes = (uint32_t*)(smem + off[L_OBYTES]);
     e.win = smem + off[L_WIN];
-    e.tp = (uint16_t*)(smem + off[L_WIN]);   // tempPrices only live inside fill_distances_prices
-    if constexpr (SOLO) {
-#pragma unroll
-        for (int k = 0; k < kSV; k++) {   // Optimal() fields start at 0 (Optimal.java:3-19)
-            e.r_price.r[k] = e.r_pp.r[k] = e.r_bp.r[k] = e.r_bp2.r[k] = e.r_fs.r[k] = e.r_bytes.r[k] = 0;
-            e.r_backs[0].r[k] = e.r_backs[1].r[k] = e.r_backs[2].r[k] = e.r_backs[3].r[k] = 0;
-        }
-#pragma unroll
-        for (int sd = 0; sd < kSides; sd++)
-#pragma unroll
-            for (int it = 0; it < kGI; it++) e.g_win[sd][it] = 0;
-    }
     e.rbuf = (uint16_t*)(smem + off[L_RBUF]);
     uint8_t* scratch = a.scratch + (size_t)blockIdx.x * a.scratch_stride;
     e.spill = __builtin_amdgcn_make_buffer_rsrc(scratch, 0, kNumOpts * 4 * 10, 0x00020000);
@@ -1665,48 +1431,28 @@ __device__ __forceinline__ void enc_body(const EncArgs& a) {
     }
 }
 
-template <typename PairT, bool LIT_LDS, int PBS, int SPEC>
-__global__ void __launch_bounds__(kWave, 4) enc_kernel(EncArgs a) {   // batch: 16 streams per CU
-    enc_body<PairT, LIT_LDS, PBS, SPEC, false>(a);
-}
-
-// Solo: at most kSoloPerCu streams per CU (nstreams <= kSoloStreams), one wave per SIMD
-// with the whole register file, so the _optimum slots and the gather window stay in
-// registers and the literal coders in LDS: per-stream latency first (config 4's long
-// streams, the JNI single-stream path, strong scaling's small per-rank shares).
-template <typename PairT, bool LIT_LDS, int PBS, int SPEC>
-__global__ void __launch_bounds__(kWave, 1) enc_kernel_solo(EncArgs a) {
-    enc_body<PairT, LIT_LDS, PBS, SPEC, true>(a);
-}
-
 size_t enc_lds_bytes(const EncArgs& a) { return enc_lds_layout(a, nullptr); }
 
 size_t enc_scratch_per_block(const Derived&) { return (size_t)kNumOpts * 4 * 10 + 256; }
 
 size_t enc_lit_bytes(const Derived& d) { return ((size_t)0x300 << (d.lc + d.lp)) * 2 + 2; }   // + the sink entry
 
-uint32_t enc_lit_in_lds(const Derived& d, bool solo) {
-    return (d.lc + d.lp) <= (uint32_t)(solo ? kLitLdsMaxBitsSolo : kLitLdsMaxBits);
-}
+uint32_t enc_lit_in_lds(const Derived& d) { return (d.lc + d.lp) <= (uint32_t)kLitLdsMaxBits; }
 
 int enc_grid(const Derived&, int nstreams) { return nstreams; }   // one workgroup per stream
 
 template <typename PairT, bool LIT, int PBS, int SPEC>
 static void launch_spec(Ctx* ctx, const EncArgs& a, int grid, size_t lds, hipStream_t st) {
-    const void* fn = a.solo ? (const void*)enc_kernel_solo<PairT, LIT, PBS, SPEC> : (const void*)enc_kernel<PairT, LIT, PBS, SPEC>;
-    if (lds > 64 * 1024) hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (lds > 64 * 1024)
+        hipFuncSetAttribute((const void*)enc_kernel<PairT, LIT, PBS, SPEC>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     TimedLaunch tl(ctx, "enc_parse", st);
-    if (a.solo) hipLaunchKernelGGL((enc_kernel_solo<PairT, LIT, PBS, SPEC>), dim3(grid), dim3(kWave), lds, st, a);
-    else hipLaunchKernelGGL((enc_kernel<PairT, LIT, PBS, SPEC>), dim3(grid), dim3(kWave), lds, st, a);
+    hipLaunchKernelGGL((enc_kernel<PairT, LIT, PBS, SPEC>), dim3(grid), dim3(kWave), lds, st, a);
 }
 
 template <typename PairT, bool LIT, int PBS>
 static void launch_one(Ctx* ctx, const EncArgs& a, int grid, size_t lds, hipStream_t st) {
-    // the level-5 parameters specialised: the batch kernel's (u32 pairs, HBM literal coders) and
-    // the solo kernel's (LDS literal coders, either pair width)
-    constexpr bool spec_ok = PBS == 2 && (std::is_same<PairT, uint32_t>::value ? !LIT : LIT);
-    if constexpr (spec_ok) {
-        if (a.fb == 32 && a.lc == 3 && a.lp == 0 && a.pb == 2 && a.eos == 0 && (a.solo != 0) == LIT) {
+    if constexpr (std::is_same<PairT, uint32_t>::value && !LIT && PBS == 2) {
+        if (a.fb == 32 && a.lc == 3 && a.lp == 0 && a.pb == 2 && a.eos == 0) {
             launch_spec<PairT, LIT, PBS, 1>(ctx, a, grid, lds, st);
             return;
         }

@@ -16,13 +16,6 @@
 #define LZG_WAVE 64
 #endif
 
-// v_writelane_b32 (no clang builtin exists for it): the LLVM intrinsic by its symbol name
-#if LZG_WAVE == 64
-__device__ int lzg_writelane(int val, int lane, int old) __asm("llvm.amdgcn.writelane.i32");
-#else
-inline int lzg_writelane(int val, int, int) { return val; }   // wave width 1 (CPU emulation): the only lane
-#endif
-
 namespace lzg {
 
 constexpr int kWave = LZG_WAVE;

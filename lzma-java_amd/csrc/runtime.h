@@ -96,11 +96,6 @@ struct Ctx {
     DevBuf io_in, io_out, io_pack, io_offs;
     std::string err;
     bool debug = getenv("LZMA_MI355X_DEBUG") != nullptr;   // phase trace on stderr (synchronises)
-    // parse kernel choice: 0 = by stream count (solo when <= kSoloPerCu per CU), 1 = always the
-    // batch kernel, 2 = always the solo kernel (LZMA_MI355X_ENC=batch|solo; tests cover both)
-    int enc_mode = getenv("LZMA_MI355X_ENC") ? (strcmp(getenv("LZMA_MI355X_ENC"), "batch") == 0 ? 1
-                                                : strcmp(getenv("LZMA_MI355X_ENC"), "solo") == 0 ? 2 : 0) : 0;
-    int cus = 0;                  // compute units of the device (hipDeviceAttributeMultiprocessorCount)
     uint64_t batch_bytes = 512ull << 20;
     // persistent workspace arena (grown, never shrunk)
     uint8_t* arena = nullptr;
@@ -281,7 +276,6 @@ struct EncArgs {
     uint32_t fb, lc, lp, pb, eos, dist_table_size, len_table_size;
     uint32_t lit_in_lds;
     uint32_t pair_bytes;          // 4 (u32 packed pairs) or 8 (u64, streams >= 8 MiB)
-    uint32_t solo;                // 1: the solo kernel (enc.hip enc_kernel_solo), 0: the batch kernel
     uint32_t* dbg;                // debug checkpoints (host-mapped, LZMA_MI355X_DEBUG only) or null
     uint64_t* prof;               // phase cycles [nstreams][kProfSlots] (LZG_PROF builds) or null
 };
@@ -311,9 +305,7 @@ int launch_rc(Ctx* ctx, const RcArgs& a, hipStream_t st);
 // records one stream of n bytes can need: <= 21 per byte (a length-2 match: isMatch, isRep,
 // 4 length bits, 6 slot bits, 30 footer bits), the end marker (42) and the first literal
 __host__ __device__ inline uint64_t rc_record_bound(uint64_t n) { return (24 * n + 64 + 63) & ~(uint64_t)63; }
-uint32_t enc_lit_in_lds(const Derived& d, bool solo);
-// the solo parse kernel runs when a pass has at most kSoloPerCu streams per CU
-constexpr int kSoloPerCu = 4;
+uint32_t enc_lit_in_lds(const Derived& d);
 size_t enc_scratch_per_block(const Derived& d);
 size_t enc_lit_bytes(const Derived& d);
 
@@ -330,14 +322,11 @@ struct DecArgs {
     unsigned int* next;
     uint8_t* scratch;             // per-block literal probs when they do not fit LDS
     uint64_t scratch_stride;
-    uint32_t lc, lp, pb, dict_check;
-    uint32_t lit_lds_coders;      // literal coders 0 .. lit_lds_coders-1 live in LDS, the rest in `scratch`
+    uint32_t lc, lp, pb, dict_check, lit_in_lds;
 };
 
 int launch_decoder(Ctx* ctx, const DecArgs& a, int grid, hipStream_t st);
-int dec_grid(int nstreams);
-// literal coders of a stream the decoder keeps in LDS when `per_cu` streams share a CU
-uint32_t dec_lit_lds_coders(uint32_t lc, uint32_t lp, uint32_t pb, int per_cu);
+int dec_grid(uint32_t lc, uint32_t lp, uint32_t lit_in_lds, int nstreams);
 int enc_grid(const Derived& d, int nstreams);
 size_t enc_lds_bytes(const EncArgs& a);
 size_t dec_scratch_per_block(uint32_t lc, uint32_t lp);

@@ -242,10 +242,7 @@ static int encode_pass(Ctx* ctx, const Derived& d, const uint8_t* d_in, const ui
         a.lit_scratch = ctx->litbuf;
         a.fb = d.fb; a.lc = d.lc; a.lp = d.lp; a.pb = d.pb; a.eos = d.eos;
         a.dist_table_size = d.dist_table_size; a.len_table_size = d.len_table_size;
-        if (ctx->cus == 0 && hipDeviceGetAttribute(&ctx->cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess)
-            ctx->cus = 256;
-        a.solo = ctx->enc_mode == 2 || (ctx->enc_mode == 0 && ns <= kSoloPerCu * ctx->cus) ? 1u : 0u;
-        a.lit_in_lds = enc_lit_in_lds(d, a.solo != 0);
+        a.lit_in_lds = enc_lit_in_lds(d);
         a.pair_bytes = wide ? 8 : 4;
         LZG_TRACE(ctx, st, "encode pass: %d streams, %llu bytes, grid %d", ns, (unsigned long long)total, grid);
         DebugWatch watch;
@@ -322,18 +319,14 @@ static int decode_batch_dev(Ctx* ctx, const uint8_t props[5], const uint8_t* d_i
     }
     uint32_t dict = (uint32_t)props[1] | ((uint32_t)props[2] << 8) | ((uint32_t)props[3] << 16) | ((uint32_t)props[4] << 24);
     const uint32_t lc = (uint32_t)p.lc, lp = (uint32_t)p.lp, pb = (uint32_t)p.pb;
+    const uint32_t lit_lds = 0;   // literal coders always in the per-stream HBM scratch (dec.hip)
     std::vector<uint32_t> order(nstreams);
     std::iota(order.begin(), order.end(), 0u);
     std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
         return (h_out_offs[a + 1] - h_out_offs[a]) > (h_out_offs[b + 1] - h_out_offs[b]);
     });
-    const int grid = dec_grid(nstreams);
-    const size_t scr = (dec_scratch_per_block(lc, lp) + 255) & ~(size_t)255;
-    if (ctx->cus == 0 && hipDeviceGetAttribute(&ctx->cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess)
-        ctx->cus = 256;
-    // one workgroup (one wave) per stream, all resident at once when they fit: the LDS a stream
-    // may use is the CU's share divided by the streams per CU
-    const int per_cu = (nstreams + ctx->cus - 1) / ctx->cus;
+    const int grid = dec_grid(lc, lp, lit_lds, nstreams);
+    const size_t scr = lit_lds ? 0 : ((dec_scratch_per_block(lc, lp) + 255) & ~(size_t)255);
     Carver probe(nullptr);
     probe.take<uint64_t>(nstreams + 1); probe.take<int64_t>(nstreams); probe.take<uint64_t>(nstreams + 1);
     probe.take<uint64_t>(nstreams); probe.take<int32_t>(nstreams); probe.take<uint32_t>(nstreams);
@@ -359,7 +352,7 @@ static int decode_batch_dev(Ctx* ctx, const uint8_t props[5], const uint8_t* d_i
     a.out_lens = d_lens; a.status = d_status; a.order = d_order; a.nstreams = nstreams; a.next = d_next;
     a.scratch = d_scr; a.scratch_stride = scr; a.lc = lc; a.lp = lp; a.pb = pb;
     a.dict_check = dict > 1 ? dict : 1;
-    a.lit_lds_coders = dec_lit_lds_coders(lc, lp, pb, per_cu);
+    a.lit_in_lds = lit_lds;
     int rc = launch_decoder(ctx, a, grid, st);
     if (rc) return rc;
     HIPCHK(hipMemcpyAsync(h_out_lens, d_lens, nstreams * 8, hipMemcpyDeviceToHost, st));

@@ -237,7 +237,6 @@ inline unsigned atomicAdd(unsigned* p, unsigned v);
 // wave width 1: the first active lane is the only lane
 inline int __builtin_amdgcn_readfirstlane(int v) { return v; }
 inline int __builtin_amdgcn_readlane(int v, int) { return v; }
-inline int __builtin_amdgcn_writelane(int v, int, int) { return v; }   // wave width 1: the only lane
 #define __builtin_nontemporal_load(p) (*(p))
 #define __builtin_nontemporal_store(v, p) (*(p) = (v))
 struct __amdgpu_buffer_rsrc_t { uint8_t* base; uint32_t bytes; };

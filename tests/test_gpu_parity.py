@@ -28,24 +28,6 @@ def ctx():
     c.close()
 
 
-def _ctx_with_parse_kernel(kind):
-    """A context whose encoder always runs one parse kernel: 'solo' (register-resident
-    _optimum, LDS literal coders) or 'batch' (16 streams per CU). By default the stream
-    count picks it, so without this most small tests would only reach the solo kernel."""
-    os.environ["LZMA_MI355X_ENC"] = kind
-    try:
-        return lzma_amd.Context(0)
-    finally:
-        del os.environ["LZMA_MI355X_ENC"]
-
-
-@pytest.fixture(scope="module", params=["solo", "batch"])
-def ectx(request):
-    c = _ctx_with_parse_kernel(request.param)
-    yield c
-    c.close()
-
-
 def _oparams(p):
     return orc.params(p.dict_size, p.fb, p.mf, p.lc, p.lp, p.pb, p.eos)
 
@@ -82,13 +64,13 @@ def firefox():
 
 
 @pytest.mark.parametrize("case", _GOLDENS, ids=[" ".join(c["switches"]) or "default" for c in _GOLDENS])
-def test_gpu_lzma_alone_golden(ectx, firefox, case):
+def test_gpu_lzma_alone_golden(ctx, firefox, case):
     """LzmaAloneTest.java:25-39 on the GPU: md5 + length of the .lzma file and the round trip."""
     p = _switch_params(case["switches"])
-    blob = lzma_amd.compress_file_bytes(firefox, p, ectx)
+    blob = lzma_amd.compress_file_bytes(firefox, p, ctx)
     assert len(blob) == case["len"]
     assert hashlib.md5(blob).hexdigest() == case["md5"]
-    assert lzma_amd.decompress_file_bytes(blob, ectx) == firefox
+    assert lzma_amd.decompress_file_bytes(blob, ctx) == firefox
 
 
 def _inputs(rng):
@@ -116,11 +98,11 @@ _PARAMS = [
 
 
 @pytest.mark.parametrize("pi", range(len(_PARAMS)))
-def test_gpu_encode_matches_oracle(ectx, pi):
+def test_gpu_encode_matches_oracle(ctx, pi):
     p = lzma_amd.make_params(**_PARAMS[pi])
     rng = np.random.default_rng(100 + pi)
     streams = list(_inputs(rng))
-    outs = ectx.encode_batch(streams, p)
+    outs = ctx.encode_batch(streams, p)
     for i, (s, o) in enumerate(zip(streams, outs)):
         assert o == orc.encode(s, _oparams(p)), "stream %d (len %d)" % (i, len(s))
 
@@ -137,7 +119,7 @@ def test_gpu_decode_matches_oracle(ctx, pi):
         assert st == lzma_amd.LZMA_OK and dec == s
 
 
-def test_gpu_many_streams_bench_chunks(ectx):
+def test_gpu_many_streams_bench_chunks(ctx):
     """Config-5 shape in miniature: many independent BENCH chunks of ragged sizes, L5 params."""
     data = lzma_amd.bench_generate(3 << 20).tobytes()
     rng = np.random.default_rng(5)
@@ -145,19 +127,19 @@ def test_gpu_many_streams_bench_chunks(ectx):
     cuts = np.concatenate([[0], cuts, [len(data)]])
     streams = [data[cuts[i]:cuts[i + 1]] for i in range(len(cuts) - 1)]
     p = lzma_amd.make_params(dict_size=1 << 18, fb=32)
-    outs = ectx.encode_batch(streams, p)
+    outs = ctx.encode_batch(streams, p)
     for i in range(0, len(streams), 7):   # oracle on a deterministic subset keeps this test in seconds
         assert outs[i] == orc.encode(streams[i], _oparams(p)), i
-    dec = ectx.decode_batch(outs, lzma_amd.write_props(p), [len(s) for s in streams])
+    dec = ctx.decode_batch(outs, lzma_amd.write_props(p), [len(s) for s in streams])
     for s, (st, d) in zip(streams, dec):
         assert st == lzma_amd.LZMA_OK and d == s
 
 
-def test_gpu_wide_pairs_stream_over_8mib(ectx):
+def test_gpu_wide_pairs_stream_over_8mib(ctx):
     """A stream > 8 MiB switches match pairs to 64-bit packing."""
     data = lzma_amd.bench_generate(9 << 20).tobytes()
     p = lzma_amd.make_params(dict_size=1 << 24, fb=32)
-    out = ectx.encode_batch([data], p)[0]
+    out = ctx.encode_batch([data], p)[0]
     assert out == orc.encode(data, _oparams(p))
 
 
@@ -275,7 +257,7 @@ def test_gpu_match_lists_equal_oracle(ctx, name, kw, gen):
         assert (counts > 4).mean() > 1 / 8   # the case really overflows the first pool
 
 
-def test_gpu_overflow_retry_encode_equals_oracle(ectx):
+def test_gpu_overflow_retry_encode_equals_oracle(ctx):
     """The encoder consumes the regrown overflow pool: bytes equal Encoder.Code."""
     data = np.random.default_rng(4).integers(0, 4, 150000, dtype=np.uint8).tobytes()
     p = lzma_amd.make_params(dict_size=1 << 20, fb=273, mf=1)
@@ -290,24 +272,24 @@ def test_gpu_overflow_retry_encode_equals_oracle(ectx):
 
 # ---------------------------------------------------------------- BASELINE.json configs at their own shapes
 
-def test_gpu_config1_rnd_1mib_lzma_alone_defaults(ectx):
+def test_gpu_config1_rnd_1mib_lzma_alone_defaults(ctx):
     """Config 1: 1 MiB of SplitMix64 bytes (seed 0x5EED) at LzmaAlone defaults
     (d23 fb128 bt4 lc3 lp0 pb2): GPU bytes equal Encoder.Code's, and the round trip."""
     data = lzma_amd.rnd_generate(1 << 20, 0x5EED).tobytes()
     p = lzma_amd.make_params(dict_size=1 << 23, fb=128, mf=1)
-    blob = lzma_amd.compress_file_bytes(data, p, ectx)
+    blob = lzma_amd.compress_file_bytes(data, p, ctx)
     assert blob == orc.lzma_file(data, _oparams(p))
-    assert lzma_amd.decompress_file_bytes(blob, ectx) == data
+    assert lzma_amd.decompress_file_bytes(blob, ctx) == data
 
 
-def test_gpu_config2_shape_256_streams_l5_every_stream(ectx):
+def test_gpu_config2_shape_256_streams_l5_every_stream(ctx):
     """Config 2's stream shape: 256 independent 256 KiB BENCH streams (64 MiB) at
     dict 2^26 L5 (fb32 bt4 lc3 lp0 pb2), every stream byte-equal to the oracle."""
     chunk = 256 << 10
     data = lzma_amd.bench_generate(256 * chunk)
     streams = [data[i:i + chunk] for i in range(0, data.size, chunk)]
     p = lzma_amd.make_params(dict_size=1 << 26, fb=32, mf=1)
-    outs = ectx.encode_batch(streams, p)
+    outs = ctx.encode_batch(streams, p)
     ref = orc.encode_many([s.tobytes() for s in streams], _oparams(p))
     bad = [i for i, (o, r) in enumerate(zip(outs, ref)) if o != r]
     assert not bad, "streams differ: %s" % bad[:10]

@@ -15,4 +15,4 @@ for w in $what; do
     esac
   done
 done
-cat $O/solo.jsonl $O/ab.jsonl 2>/dev/null
+cat $O/solo.jsonl $O/ab.jsonl 2>/dev/null || true
