@@ -413,9 +413,16 @@ struct Dec {
     }
 };
 
+// LDS of one stream: fixed models, input ring, output window (16-byte aligned regions)
+template <int PBS>
+constexpr size_t kDecLdsBytes = (((size_t)ProbLayout<PBS>::COUNT * 2 + 15) & ~(size_t)15) + kIbuf + kWin;
+
 template <int PBS>
 __global__ void __launch_bounds__(kWave) dec_kernel(DecArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    // a static LDS array (the layout is fixed per PBS): its address is known when the kernel
+    // is compiled, so LDS offsets fold into the ds instructions (a dynamic extern array's
+    // base is a link-time constant that costs an s_add per address computation)
+    __shared__ __attribute__((aligned(16))) uint8_t smem[kDecLdsBytes<PBS>];
     Dec<PBS> d;
     d.lane = threadIdx.x;
     d.lc = a.lc; d.lp = a.lp; d.pb = a.pb; d.ps_mask = (1u << a.pb) - 1; d.dict_check = a.dict_check;
@@ -452,7 +459,8 @@ int dec_grid(uint32_t, uint32_t, uint32_t, int nstreams) { return nstreams; }   
 
 template <int PBS>
 static void launch_dec(const DecArgs& a, int grid, size_t lds, hipStream_t st) {
-    hipLaunchKernelGGL((dec_kernel<PBS>), dim3(grid), dim3(kWave), lds, st, a);
+    (void)lds;   // static LDS (kDecLdsBytes)
+    hipLaunchKernelGGL((dec_kernel<PBS>), dim3(grid), dim3(kWave), 0, st, a);
 }
 
 int launch_decoder(Ctx* ctx, const DecArgs& a, int grid, hipStream_t st) {
