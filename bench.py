@@ -65,8 +65,9 @@ def parse():
     ap.add_argument("--single-stream", type=int, default=16 << 20,
                     help="bytes of the one-stream measurement after the timed region (SURVEY 7.3's serial tail, "
                          "config 4's regime): GPU encode/decode of one stream beside the oracle on 1 thread (0 = skip)")
-    ap.add_argument("--parity-streams", type=int, default=16,
-                    help="streams each rank checks against the oracle when there is no cpu_baseline sample")
+    ap.add_argument("--parity-streams", type=int, default=-1,
+                    help="streams each rank checks against the oracle (-1 = every stream; at N=1 the "
+                         "cpu_baseline sample's oracle bytes are reused and the rest encoded beside them)")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--overlap", action="store_true",
                     help="pipeline the steps: the decode of step k runs on its own HIP stream and context while "
@@ -225,10 +226,12 @@ def main():
         chunks = [host[int(offs[i]):int(offs[i + 1])] for i in range(n)]
         if rank == 0 and world == 1 and args.cpu_sample > 0:
             cpu, ref = cpu_baseline(orc, op, chunks, args)
-        elif not args.no_verify:
-            idx = spread(n, args.parity_streams)
-            outs = orc.encode_many([chunks[i].tobytes() for i in idx], op, threads=min(4, orc.cpu_threads()))
-            ref = dict(zip(idx, outs))
+        if not args.no_verify:
+            want = range(n) if args.parity_streams < 0 else spread(n, args.parity_streams)
+            idx = [i for i in want if i not in ref]
+            if idx:   # not timed: the parity check of the streams the baseline sample did not cover
+                outs = orc.encode_many([chunks[i].tobytes() for i in idx], op, threads=orc.cpu_threads())
+                ref.update(zip(idx, outs))
     parity_ok, checked = True, 0
     if ref:
         host_pack = state["buf"][:comp_bytes].cpu().numpy()

@@ -282,11 +282,12 @@ def test_gpu_config1_rnd_1mib_lzma_alone_defaults(ctx):
     assert lzma_amd.decompress_file_bytes(blob, ctx) == data
 
 
-def test_gpu_config2_shape_256_streams_l5_every_stream(ctx):
-    """Config 2's stream shape: 256 independent 256 KiB BENCH streams (64 MiB) at
-    dict 2^26 L5 (fb32 bt4 lc3 lp0 pb2), every stream byte-equal to the oracle."""
+def test_gpu_config2_full_256mib_l5_every_stream(ctx):
+    """Config 2 at its full size: 256 MiB of BENCH data as 1024 independent 256 KiB
+    streams (the bench's chunking) at dict 2^26 L5 (fb32 bt4 lc3 lp0 pb2), every
+    stream byte-equal to the oracle."""
     chunk = 256 << 10
-    data = lzma_amd.bench_generate(256 * chunk)
+    data = lzma_amd.bench_generate(1024 * chunk)
     streams = [data[i:i + chunk] for i in range(0, data.size, chunk)]
     p = lzma_amd.make_params(dict_size=1 << 26, fb=32, mf=1)
     outs = ctx.encode_batch(streams, p)
@@ -331,7 +332,7 @@ def test_gpu_config5_shape_4096_streams_dict18(ctx):
 
 
 def test_gpu_config3_text_dict28(ctx):
-    """Config 3's parameters: TEXT input at dict 2^28 (hashMask 0x3FFFFFF: 26 hash
+    """Config 3's parameters: TEXT data at dict 2^28 (the largest hash mask, 26
     bits in the sort keys, distTableSize 56), L5, several 2 MiB streams, every
     stream byte-equal to the oracle."""
     chunk = 2 << 20
@@ -345,6 +346,37 @@ def test_gpu_config3_text_dict28(ctx):
     dec = ctx.decode_batch(outs, lzma_amd.write_props(p), [chunk] * len(outs))
     for s, (st, d) in zip(streams, dec):
         assert st == lzma_amd.LZMA_OK and d == s
+
+
+@pytest.mark.timeout(600)
+def test_gpu_config3_full_1gib_text_dict28_every_stream(ctx, heartbeat):
+    """Config 3 at its full size: 1 GiB of TEXT ("enwik9-shaped") data as 4096
+    independent 256 KiB streams (the bench's --data text chunking) at dict 2^28 L5,
+    device-resident, every stream byte-equal to the oracle and decoded back."""
+    torch = pytest.importorskip("torch")
+    chunk, n = 256 << 10, 4096
+    data = lzma_amd.text_generate(n * chunk)
+    p = lzma_amd.make_params(dict_size=1 << 28, fb=32, mf=1)
+    dev = torch.device("cuda", 0)
+    d_in = torch.from_numpy(data).to(dev)
+    offs = np.arange(n + 1, dtype=np.uint64) * np.uint64(chunk)
+    cap_offs = np.zeros(n + 1, dtype=np.uint64)
+    cap_offs[1:] = np.cumsum([lzma_amd.enc_bound(chunk)] * n)
+    d_comp = torch.empty(int(cap_offs[-1]), dtype=torch.uint8, device=dev)
+    st = torch.cuda.current_stream(dev).cuda_stream
+    ctx.set_batch_bytes(1 << 30)
+    lens = ctx.encode_batch_dev(d_in, offs, p, d_comp, cap_offs, st)
+    d_pack = torch.empty(int(lens.sum()) + 1, dtype=torch.uint8, device=dev)
+    pk = ctx.pack_dev(d_comp, cap_offs, lens, d_pack, st)
+    d_dec = torch.zeros(n * chunk, dtype=torch.uint8, device=dev)
+    dlens, dst = ctx.decode_batch_dev(lzma_amd.write_props(p), d_pack, pk, np.full(n, chunk, dtype=np.int64),
+                                      d_dec, offs, st)
+    assert (dst == 0).all() and (dlens == chunk).all()
+    assert torch.equal(d_dec, d_in)
+    host_pack = d_pack.cpu().numpy()
+    ref = orc.encode_many([data[i * chunk:(i + 1) * chunk].tobytes() for i in range(n)], _oparams(p))
+    bad = [i for i in range(n) if host_pack[int(pk[i]):int(pk[i + 1])].tobytes() != ref[i]]
+    assert not bad, "streams differ: %s" % bad[:10]
 
 
 def test_gpu_single_stream_c_abi(ctx):
