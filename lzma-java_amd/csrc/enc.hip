@@ -22,8 +22,10 @@
 //   * the per-stream state struct holds scalars and LDS pointers only (no
 //     arrays), and every member is force-inlined, so it lives in registers;
 //   * probability models, price tables, the match-info prefetch ring and
-//     the first kOptLds _optimum entries (SoA) live in LDS; deeper _optimum
-//     entries spill to a per-block HBM scratch behind an explicit fence;
+//     kOptLds _optimum entries (SoA) live in LDS: with fb <= 32 (RING) a
+//     ring of the slots around the forward loop's position, whose evicted
+//     entries go to a per-block HBM home; with fb > 32 the first kOptLds
+//     slots, deeper ones in that HBM scratch behind an explicit fence;
 //   * lanes exchange data through LDS only; a wavefront-scope fence orders
 //     the compiler (LDS executes one wave's ops in order).
 #include "lzma_common.h"
@@ -37,6 +39,9 @@ static __constant__ Tables c_tab = make_tables();
 
 constexpr int kOptLds = 64;         // _optimum slots kept in LDS (deeper slots spill to HBM); the LDS arrays
                                     // have one more slot, kOptLds, a sink for the writes of idle lanes
+constexpr uint32_t kOptMask = kOptLds - 1;   // RING: slot i lives in entry i & kOptMask
+constexpr uint32_t kFarEntry = kOptLds + 1;   // RING: the entry of slot cur + 65 until cur + 1 retires
+static_assert((kOptLds & (kOptLds - 1)) == 0, "the _optimum ring is a power of two");
 constexpr int kLitLdsMaxBits = 1;   // literal coders in LDS when lc + lp <= 1 (<= 3 KiB); else HBM/L2
 constexpr int kMdCap = kMatchMaxLen + 1;
 constexpr int kRing = 32;           // match-info prefetch window (positions)
@@ -118,7 +123,7 @@ FI uint32_t sel4(uint32_t i, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
 // FairPrio rows of the encoder's waves (lzma_common.h)
 __device__ uint32_t g_enc_sched[kSchedRows * kSchedCols];
 
-template <typename PairT, bool LIT_LDS, int PBS>
+template <typename PairT, bool LIT_LDS, int PBS, bool RING>
 struct Enc {
     using PP = PairPack<PairT>;
     using PL = ProbLayout<PBS>;
@@ -143,14 +148,14 @@ struct Enc {
     uint32_t* md_dist;
     uint32_t* ring_info;      // [kRing]
     PairT* ring_pairs;        // [kRing * kInlinePairs]
-    uint32_t* o_price;        // _optimum SoA, [kOptLds] each
+    uint32_t* o_price;        // _optimum SoA, [kOptLds] each (+ the sink entry, + kFarEntry)
     uint32_t* o_pp;
     int32_t* o_bp;
     int32_t* o_bp2;
     uint8_t* o_fs;
     uint32_t* o_backs;        // [4][kOptLds]
     uint32_t* o_bytes;        // [kOptLds] cur byte | match byte << 8 | previous byte << 16 of each parsed
-                              // position, so the coder needs no HBM byte loads
+                              // position, so the coder needs no HBM byte loads (RING: | state << 24)
     uint8_t* win;             // gather window [kSides][kGW]: cur side, reps 0-3, pairs 0-1
     uint16_t* rbuf;           // coder-record staging ring [kRbuf]
     __amdgpu_buffer_rsrc_t spill;   // _optimum slots >= kOptLds in HBM (9 fields x kNumOpts dwords)
@@ -179,6 +184,9 @@ struct Enc {
     uint32_t rd0, rd1, rd2, rd3;   // _repDistances
     uint32_t rp0, rp1, rp2, rp3;   // reps
     uint32_t match_price_count, align_price_count;
+    // ---- RING bookkeeping of _optimum (see the accessors)
+    uint32_t ring_top;        // highest slot whose ahead fields are in the ring
+    uint32_t far_valid;       // slot cur + 65 is held in the far entry (kFarEntry)
     FairPrio prio;
     // ---- per-position gather (see gather()): p = current position, equality masks per side
     uint32_t gp;
@@ -198,25 +206,63 @@ struct Enc {
     FI void sstore(uint32_t field, uint32_t i, uint32_t v) {
         __builtin_amdgcn_raw_buffer_store_b32(v, spill, (field * kNumOpts + i) * 4, 0, 0);
     }
-    template <bool F = false> FI uint32_t price_at(uint32_t i) const { if (F || i < (uint32_t)kOptLds) return o_price[i]; return sload(0, i); }
-    template <bool F = false> FI void set_price(uint32_t i, uint32_t v) { if (F || i < (uint32_t)kOptLds) o_price[i] = v; else sstore(0, i, v); }
-    template <bool F = false> FI uint32_t pp_at(uint32_t i) const { if (F || i < (uint32_t)kOptLds) return o_pp[i]; return sload(1, i); }
-    template <bool F = false> FI void set_pp(uint32_t i, uint32_t v) { if (F || i < (uint32_t)kOptLds) o_pp[i] = v; else sstore(1, i, v); }
-    template <bool F = false> FI int32_t bp_at(uint32_t i) const { if (F || i < (uint32_t)kOptLds) return o_bp[i]; return (int32_t)sload(2, i); }
-    template <bool F = false> FI void set_bp(uint32_t i, int32_t v) { if (F || i < (uint32_t)kOptLds) o_bp[i] = v; else sstore(2, i, (uint32_t)v); }
-    template <bool F = false> FI int32_t bp2_at(uint32_t i) const { if (F || i < (uint32_t)kOptLds) return o_bp2[i]; return (int32_t)sload(3, i); }
-    template <bool F = false> FI void set_bp2(uint32_t i, int32_t v) { if (F || i < (uint32_t)kOptLds) o_bp2[i] = v; else sstore(3, i, (uint32_t)v); }
-    template <bool F = false> FI uint32_t fs_at(uint32_t i) const { if (F || i < (uint32_t)kOptLds) return (uint32_t)o_fs[i]; return sload(4, i); }
-    template <bool F = false> FI void set_fs(uint32_t i, uint32_t v) { if (F || i < (uint32_t)kOptLds) o_fs[i] = (uint8_t)v; else sstore(4, i, v); }
-    template <bool F = false> FI uint32_t back_at(uint32_t i, int k) const {
-        if (F || i < (uint32_t)kOptLds) return o_backs[k * kOptLds + i];
+    // Which copy of slot i is current. Non-RING (fb > 32): slots < kOptLds in
+    // LDS, deeper ones in HBM. RING (fb <= 32): one forward step reads slots
+    // >= cur - 65 and writes slots <= cur + 65 (lenTest, lenTest2 <= fb), so
+    // LDS holds a ring: the "ahead" fields (price, pp, bp, bp2, flags) of the
+    // slots (ring_top - 64, ring_top] and the "behind" fields (backs, bytes |
+    // state << 24) of (top - 64, top], top the last slot a step wrote. An
+    // entry is written back to the slot's HBM home (field layout as the spill
+    // scratch) before the ring reuses it; Backward, the cached path and the
+    // coder read older slots there. F: the caller knows the slot is in LDS.
+    FI bool a_in(uint32_t i) const { return RING ? i + (uint32_t)kOptLds > ring_top : i < (uint32_t)kOptLds; }
+    // top: the highest slot whose behind fields were written (cur - 1 in a forward
+    // step, opt_end - 1 once the parse has ended)
+    FI bool b_in(uint32_t i, uint32_t top) const { return RING ? i + (uint32_t)kOptLds > top : i < (uint32_t)kOptLds; }
+    static FI uint32_t ix(uint32_t i) { return RING ? (i & kOptMask) : i; }
+    template <bool F = false> FI uint32_t price_at(uint32_t i) const { if (F || a_in(i)) return o_price[ix(i)]; return sload(0, i); }
+    template <bool F = false> FI void set_price(uint32_t i, uint32_t v) { if (F || a_in(i)) o_price[ix(i)] = v; else sstore(0, i, v); }
+    template <bool F = false> FI uint32_t pp_at(uint32_t i) const { if (F || a_in(i)) return o_pp[ix(i)]; return sload(1, i); }
+    template <bool F = false> FI void set_pp(uint32_t i, uint32_t v) { if (F || a_in(i)) o_pp[ix(i)] = v; else sstore(1, i, v); }
+    template <bool F = false> FI int32_t bp_at(uint32_t i) const { if (F || a_in(i)) return o_bp[ix(i)]; return (int32_t)sload(2, i); }
+    template <bool F = false> FI void set_bp(uint32_t i, int32_t v) { if (F || a_in(i)) o_bp[ix(i)] = v; else sstore(2, i, (uint32_t)v); }
+    template <bool F = false> FI int32_t bp2_at(uint32_t i) const { if (F || a_in(i)) return o_bp2[ix(i)]; return (int32_t)sload(3, i); }
+    template <bool F = false> FI void set_bp2(uint32_t i, int32_t v) { if (F || a_in(i)) o_bp2[ix(i)] = v; else sstore(3, i, (uint32_t)v); }
+    template <bool F = false> FI uint32_t fs_at(uint32_t i) const { if (F || a_in(i)) return (uint32_t)o_fs[ix(i)]; return sload(4, i); }
+    template <bool F = false> FI void set_fs(uint32_t i, uint32_t v) { if (F || a_in(i)) o_fs[ix(i)] = (uint8_t)v; else sstore(4, i, v); }
+    // behind fields: in RING mode a home read waits for the write-backs (rare: a
+    // path back by 65 slots, or a coded literal 64 slots behind the parse end)
+    template <bool F = false> FI uint32_t back_at(uint32_t i, int k, uint32_t top) const {
+        if (F || b_in(i, top)) return o_backs[k * kOptLds + ix(i)];
+        if (RING) SPILL_FENCE();
         return sload(5 + k, i);
     }
     template <bool F = false> FI void set_back(uint32_t i, int k, uint32_t v) {
-        if (F || i < (uint32_t)kOptLds) o_backs[k * kOptLds + i] = v; else sstore(5 + k, i, v);
+        if (F || RING || i < (uint32_t)kOptLds) o_backs[k * kOptLds + ix(i)] = v; else sstore(5 + k, i, v);
     }
-    template <bool F = false> FI uint32_t bytes_at(uint32_t i) const { if (F || i < (uint32_t)kOptLds) return o_bytes[i]; return sload(9, i); }
-    template <bool F = false> FI void set_bytes(uint32_t i, uint32_t v) { if (F || i < (uint32_t)kOptLds) o_bytes[i] = v; else sstore(9, i, v); }
+    template <bool F = false> FI uint32_t bytes_at(uint32_t i, uint32_t top) const {
+        if (F || b_in(i, top)) return o_bytes[ix(i)];
+        if (RING) SPILL_FENCE();
+        return sload(9, i);
+    }
+    template <bool F = false> FI void set_bytes(uint32_t i, uint32_t v) {
+        if (F || RING || i < (uint32_t)kOptLds) o_bytes[ix(i)] = v; else sstore(9, i, v);
+    }
+    // the State of slot i's best path
+    template <bool F = false> FI uint32_t state_at(uint32_t i, uint32_t top) const { return RING ? bytes_at<F>(i, top) >> 24 : fs_at<F>(i) >> 4; }
+    // RING: write back the ahead fields of slot i (its entry is about to hold i + 64)
+    FI void evict_ahead(uint32_t i) {
+        const uint32_t r = i & kOptMask;
+        LANE_FOR(uint32_t, k, 0u, 4u) {
+            const uint32_t v = k == 0 ? o_pp[r] : (k == 1 ? (uint32_t)o_bp[r] : (k == 2 ? (uint32_t)o_bp2[r] : (uint32_t)o_fs[r]));
+            sstore(1 + k, i, v);
+        }
+    }
+    // RING: write back the behind fields of slot i
+    FI void evict_behind(uint32_t i) {
+        const uint32_t r = i & kOptMask;
+        LANE_FOR(uint32_t, k, 0u, 5u) sstore(5 + k, i, k < 4 ? o_backs[k * kOptLds + r] : o_bytes[r]);
+    }
     // the gather window's bytes of the current position (see gather())
     FI uint32_t win_bytes() const { return (uint32_t)win[1] | ((uint32_t)win[kGW + 1] << 8) | ((uint32_t)win[0] << 16); }
     template <bool F = false> FI uint32_t pos_prev(uint32_t i) const { return pp_at<F>(i) & 0xFFFFu; }
@@ -224,7 +270,9 @@ struct Enc {
     // after lanes wrote slots up to `hi`, make them visible to every lane
     FI void fence_upto(uint32_t hi) {
         LANE_FENCE();
-        if (hi >= (uint32_t)kOptLds) SPILL_FENCE();
+#ifndef LZG_ABL_NOFENCE
+        if (!RING && hi >= (uint32_t)kOptLds) SPILL_FENCE();
+#endif
     }
 
     // ------------------------------------------------------------ prices
@@ -622,6 +670,7 @@ struct Enc {
                 md_dist[k] = PP::dist(pr);
             }
         } else {
+            PCOUNT(PF_NOVF);
             LANE_FOR(uint32_t, k, 0u, cnt) {
                 PairT pr = k < (uint32_t)kInlinePairs ? ring_pairs[slot * kInlinePairs + k]
                                                       : ovf[(uint64_t)ovf_off[gbase + q] * ovf_stride(fb) + k - kInlinePairs];
@@ -666,8 +715,38 @@ struct Enc {
         return dist_price(pos, len) + len_price(0, len - kMatchMinLen, ps);
     }
     // while (lenEnd < target) _optimum[++lenEnd].Price = kIfinityPrice
-    FI void extend_to(uint32_t& len_end, uint32_t target) {
+    FI void extend_to(uint32_t& len_end, uint32_t target, uint32_t cur) {
         if (len_end >= target) return;
+        if (RING) {
+            if (target > cur + (uint32_t)kOptLds + 1) { bad = 8; return; }   // beyond cur + 2 fb + 1
+            uint32_t hi = target;
+            if (hi > cur + (uint32_t)kOptLds) {   // cur + 65: its entry still holds cur + 1
+                far_valid = 1;
+                o_price[kFarEntry] = kInfinityPrice; o_pp[kFarEntry] = 0; o_bp[kFarEntry] = 0; o_bp2[kFarEntry] = 0;
+                o_fs[kFarEntry] = 0;
+                hi--;
+            }
+            if (hi >= (uint32_t)kOptLds) {   // entries reused: write back slots i - 64 first
+                LANE_FOR(uint32_t, i, len_end + 1, hi + 1) {
+                    const uint32_t r = i & kOptMask;
+                    if (i >= (uint32_t)kOptLds) {
+                        const uint32_t h = i - (uint32_t)kOptLds;
+                        sstore(1, h, o_pp[r]); sstore(2, h, (uint32_t)o_bp[r]); sstore(3, h, (uint32_t)o_bp2[r]);
+                        sstore(4, h, (uint32_t)o_fs[r]);
+                    }
+                    o_price[r] = kInfinityPrice;
+                }
+            } else {
+                for (uint32_t i0 = len_end + 1; i0 <= hi; i0 += kWave) {
+                    const uint32_t i = i0 + lane;
+                    o_price[i <= hi ? i : (uint32_t)kOptLds] = kInfinityPrice;
+                }
+            }
+            if (hi > ring_top) ring_top = hi;
+            len_end = target;
+            LANE_FENCE();
+            return;
+        }
         if (target < (uint32_t)kOptLds) {   // branch-free: idle lanes write the sink slot
             for (uint32_t i0 = len_end + 1; i0 <= target; i0 += kWave) {
                 const uint32_t i = i0 + lane;
@@ -684,12 +763,12 @@ struct Enc {
     // lanes relax slots base+l, l in [lo, hi], with a rep of index ri
     FI void relax_rep(uint32_t base_slot, uint32_t lo, uint32_t hi, uint32_t price_base, uint32_t ps,
                       uint32_t pos_prev_v, uint32_t ri) {
-        if (base_slot + hi < (uint32_t)kOptLds) {   // all slots in LDS: no per-lane spill branches
+        if (RING || base_slot + hi < (uint32_t)kOptLds) {   // all slots in LDS: no per-lane spill branches
             // branch-free: idle lanes and lanes that do not improve write the sink slot
             for (uint32_t l0 = lo; l0 <= hi; l0 += kWave) {
                 const uint32_t l = l0 + lane;
                 const bool ok = l <= hi;
-                const uint32_t s = ok ? base_slot + l : (uint32_t)kOptLds;
+                const uint32_t s = ok ? ix(base_slot + l) : (uint32_t)kOptLds;
                 const uint32_t cl = price_base + len_price(1, ok ? l - 2 : 0u, ps);
                 const uint32_t op = o_price[s], opp = o_pp[s], ofs = o_fs[s];
                 const uint32_t t = (ok && cl < op) ? s : (uint32_t)kOptLds;
@@ -716,11 +795,11 @@ struct Enc {
     // lanes relax slots base+l, l in [lo, hi], all with the match distance `dist`
     FI void relax_match(uint32_t base_slot, uint32_t lo, uint32_t hi, uint32_t price_base, uint32_t dist, uint32_t ps,
                         uint32_t pos_prev_v) {
-        if (base_slot + hi < (uint32_t)kOptLds) {   // all slots in LDS; branch-free as relax_rep
+        if (RING || base_slot + hi < (uint32_t)kOptLds) {   // all slots in LDS; branch-free as relax_rep
             for (uint32_t l0 = lo; l0 <= hi; l0 += kWave) {
                 const uint32_t l = l0 + lane;
                 const bool ok = l <= hi;
-                const uint32_t s = ok ? base_slot + l : (uint32_t)kOptLds;
+                const uint32_t s = ok ? ix(base_slot + l) : (uint32_t)kOptLds;
                 const uint32_t cl = price_base + pos_len_price(dist, ok ? l : (uint32_t)kMatchMinLen, ps);
                 const uint32_t op = o_price[s], opp = o_pp[s], ofs = o_fs[s];
                 const uint32_t t = (ok && cl < op) ? s : (uint32_t)kOptLds;
@@ -799,7 +878,24 @@ struct Enc {
         fence_upto(s);
     }
 
-    FI void relax_two_step(uint32_t s, uint32_t cl, uint32_t pos_prev_v, bool prev2, uint32_t pos_prev2_v, int32_t back2) {
+    FI void relax_two_step(uint32_t s, uint32_t cl, uint32_t pos_prev_v, bool prev2, uint32_t pos_prev2_v, int32_t back2,
+                           uint32_t cur) {
+        PCOUNT(PF_NTWO);
+        if (RING) {
+            if (far_valid && s == cur + (uint32_t)kOptLds + 1) {   // slot cur + 65: the far entry
+                const uint32_t e = kFarEntry;
+                if (cl < o_price[e]) {
+                    o_price[e] = cl;
+                    o_bp[e] = 0;
+                    if (prev2) { o_pp[e] = pos_prev_v | (pos_prev2_v << 16); o_fs[e] = (uint8_t)((o_fs[e] & ~3u) | 3u); o_bp2[e] = back2; }
+                    else { o_pp[e] = (o_pp[e] & 0xFFFF0000u) | pos_prev_v; o_fs[e] = (uint8_t)((o_fs[e] & ~3u) | 1u); }
+                }
+                LANE_FENCE();
+                return;
+            }
+            relax_two_step_t<true>(s, cl, pos_prev_v, prev2, pos_prev2_v, back2);
+            return;
+        }
         if (s < (uint32_t)kOptLds) relax_two_step_t<true>(s, cl, pos_prev_v, prev2, pos_prev2_v, back2);
         else relax_two_step_t<false>(s, cl, pos_prev_v, prev2, pos_prev2_v, back2);
     }
@@ -839,6 +935,13 @@ struct Enc {
     }
 
     FI uint32_t backward(int32_t* back_res, uint32_t cur) {   // every slot touched is <= cur
+        if (RING) {
+            if (ring_top < (uint32_t)kOptLds) return backward_t<true>(back_res, cur);
+            SPILL_FENCE();   // the write-backs before the home reads
+            const uint32_t r = backward_t<false>(back_res, cur);
+            SPILL_FENCE();   // and Backward's home writes before the cached path reads them
+            return r;
+        }
         return cur < (uint32_t)kOptLds ? backward_t<true>(back_res, cur) : backward_t<false>(back_res, cur);
     }
 
@@ -848,7 +951,7 @@ struct Enc {
             uint32_t c = (uint32_t)opt_cur;
             *sym_slot = c;
             uint32_t nxt;
-            if (c < (uint32_t)kOptLds) { nxt = pos_prev<true>(c); *back_res = bp_at<true>(c); }
+            if (a_in(c)) { nxt = pos_prev<true>(c); *back_res = bp_at<true>(c); }
             else { nxt = pos_prev(c); *back_res = bp_at(c); }
             opt_cur = (int32_t)nxt;
             if (nxt <= c || nxt > (uint32_t)opt_end) { bad = 3; return 1; }
@@ -856,6 +959,7 @@ struct Enc {
         }
         opt_cur = opt_end = 0;
         *sym_slot = 0;
+        if (RING) { ring_top = 0; far_valid = 0; }
         uint32_t len_main;
         if (longest_found) { len_main = longest_len; longest_found = 0; }
         else len_main = read_match_distances();
@@ -864,7 +968,7 @@ struct Enc {
         PCOUNT(PF_NOPT);
         PBEGIN(t0);
         gather(false);
-        set_bytes<true>(0, win_bytes());
+        set_bytes<true>(0, win_bytes() | (RING ? state << 24 : 0u));
         uint32_t num_avail = avail() + 1;
         if (num_avail < 2) { *back_res = -1; LANE_FENCE(); return 1; }
         if (num_avail > (uint32_t)kMatchMaxLen) num_avail = kMatchMaxLen;
@@ -891,7 +995,7 @@ struct Enc {
         uint32_t match_byte = b_byte(1, rp0, 0);   // rp0 == rd0 here
         if (len_main < 2 && cur_byte != match_byte && rl_max < 2) { *back_res = -1; return 1; }
 
-        set_fs<true>(0, (fs_at<true>(0) & 0xFu) | (state << 4));
+        if (!RING) set_fs<true>(0, (fs_at<true>(0) & 0xFu) | (state << 4));
         uint32_t pos_state = position & ps_mask;
         PBEGIN(t1);
         uint32_t p1 = dm0(E_IS_MATCH + (state << PBS) + pos_state) +
@@ -915,6 +1019,7 @@ struct Enc {
         PBEGIN(t2);
         if (len_end < (uint32_t)kOptLds) {
             LANE_FOR(uint32_t, l, 2u, len_end + 1) set_price<true>(l, kInfinityPrice);
+            if (RING) ring_top = len_end;
             LANE_FENCE();
         } else {
             LANE_FOR(uint32_t, l, 2u, len_end + 1) set_price(l, kInfinityPrice);
@@ -946,20 +1051,24 @@ struct Enc {
     FI bool pos_step(uint32_t cur, uint32_t position, uint32_t& st, uint32_t& pos_state, uint32_t& cur_and1,
                      uint32_t& match_price, uint32_t& rep_match_price, uint32_t& cur_byte, uint32_t& match_byte) {
         PBEGIN(ts);
-        uint32_t ppc = pp_at<F>(cur);
+        // F: cur + 1 < kOptLds, every slot touched is in LDS. RING deep steps: the
+        // ahead fields of cur and cur + 1 are in the ring (FA); the behind fields of
+        // pprev may be in HBM (a path back by 65), checked per access.
+        constexpr bool FA = F || RING, FB = F;
+        uint32_t ppc = pp_at<FA>(cur);
         uint32_t pos_prev_c = ppc & 0xFFFFu;
-        uint32_t fsc = fs_at<F>(cur);
-        int32_t bpc = bp_at<F>(cur);
+        uint32_t fsc = fs_at<FA>(cur);
+        int32_t bpc = bp_at<FA>(cur);
         uint32_t pprev = pos_prev_c;
         if (fsc & 1u) {
             pprev--;
             if (fsc & 2u) {
-                st = fs_at<F>(ppc >> 16) >> 4;
-                if (bp2_at<F>(cur) < kNumRepDistances) st = st_long(st);
+                st = state_at<FB>(ppc >> 16, cur - 1);
+                if (bp2_at<FA>(cur) < kNumRepDistances) st = st_long(st);
                 else st = st_match(st);
-            } else st = fs_at<F>(pprev) >> 4;
+            } else st = state_at<FB>(pprev, cur - 1);
             st = st_lit(st);
-        } else st = fs_at<F>(pprev) >> 4;
+        } else st = state_at<FB>(pprev, cur - 1);
         if (pprev == cur - 1) {
             if (bpc == 0) st = st_short(st);
             else st = st_lit(st);
@@ -967,14 +1076,15 @@ struct Enc {
             int32_t pos;
             if ((fsc & 1u) && (fsc & 2u)) {
                 pprev = ppc >> 16;
-                pos = bp2_at<F>(cur);
+                pos = bp2_at<FA>(cur);
                 st = st_long(st);
             } else {
                 pos = bpc;
                 if (pos < kNumRepDistances) st = st_long(st);
                 else st = st_match(st);
             }
-            uint32_t b0 = back_at<F>(pprev, 0), b1 = back_at<F>(pprev, 1), b2 = back_at<F>(pprev, 2), b3 = back_at<F>(pprev, 3);
+            uint32_t b0 = back_at<FB>(pprev, 0, cur - 1), b1 = back_at<FB>(pprev, 1, cur - 1), b2 = back_at<FB>(pprev, 2, cur - 1),
+                     b3 = back_at<FB>(pprev, 3, cur - 1);
             if (pos < kNumRepDistances) {
                 if (pos == 0) { rp0 = b0; rp1 = b1; rp2 = b2; rp3 = b3; }
                 else if (pos == 1) { rp0 = b1; rp1 = b0; rp2 = b2; rp3 = b3; }
@@ -984,14 +1094,16 @@ struct Enc {
                 rp0 = (uint32_t)(pos - kNumRepDistances); rp1 = b0; rp2 = b1; rp3 = b2;
             }
         }
-        set_fs<F>(cur, (fsc & 0xFu) | (st << 4));
-        set_back<F>(cur, 0, rp0); set_back<F>(cur, 1, rp1); set_back<F>(cur, 2, rp2); set_back<F>(cur, 3, rp3);
-        uint32_t cur_price = price_at<F>(cur);
+        if (RING) {   // cur's entry held cur - 64
+            if (!F && cur >= (uint32_t)kOptLds) evict_behind(cur - (uint32_t)kOptLds);
+        } else set_fs<FA>(cur, (fsc & 0xFu) | (st << 4));
+        set_back<FA>(cur, 0, rp0); set_back<FA>(cur, 1, rp1); set_back<FA>(cur, 2, rp2); set_back<FA>(cur, 3, rp3);
+        uint32_t cur_price = price_at<FA>(cur);
         pos_state = position & ps_mask;
         PEND(PF_STATE, ts);
         PBEGIN(tg);
         gather(true);
-        set_bytes<F>(cur, win_bytes());
+        set_bytes<FA>(cur, win_bytes() | (RING ? st << 24 : 0u));
         PEND(PF_REPLEN, tg);
         cur_byte = a_byte(0);
         match_byte = b_byte(1, rp0, 0);
@@ -1002,12 +1114,12 @@ struct Enc {
         PBEGIN(tn);
         uint32_t nx = cur + 1;
         bool next_is_char = false;
-        uint32_t nx_price = price_at<F>(nx);
-        uint32_t nx_pp = pp_at<F>(nx);
-        int32_t nx_bp = bp_at<F>(nx);
+        uint32_t nx_price = price_at<FA>(nx);
+        uint32_t nx_pp = pp_at<FA>(nx);
+        int32_t nx_bp = bp_at<FA>(nx);
         if (cur_and1 < nx_price) {
             nx_price = cur_and1; nx_pp = (nx_pp & 0xFFFF0000u) | cur; nx_bp = -1;
-            set_price<F>(nx, nx_price); set_pp<F>(nx, nx_pp); set_bp<F>(nx, -1); set_fs<F>(nx, fs_at<F>(nx) & ~1u);
+            set_price<FA>(nx, nx_price); set_pp<FA>(nx, nx_pp); set_bp<FA>(nx, -1); set_fs<FA>(nx, fs_at<FA>(nx) & ~1u);
             next_is_char = true;
         }
         match_price = cur_price + dm1(E_IS_MATCH + (st << PBS) + pos_state);
@@ -1015,7 +1127,7 @@ struct Enc {
         if (match_byte == cur_byte && !((nx_pp & 0xFFFFu) < cur && nx_bp == 0)) {
             uint32_t srp = rep_match_price + rep_len1_price(st, pos_state);
             if (srp <= nx_price) {
-                set_price<F>(nx, srp); set_pp<F>(nx, (nx_pp & 0xFFFF0000u) | cur); set_bp<F>(nx, 0); set_fs<F>(nx, fs_at<F>(nx) & ~1u);
+                set_price<FA>(nx, srp); set_pp<FA>(nx, (nx_pp & 0xFFFF0000u) | cur); set_bp<FA>(nx, 0); set_fs<FA>(nx, fs_at<FA>(nx) & ~1u);
                 next_is_char = true;
             }
         }
@@ -1045,10 +1157,23 @@ struct Enc {
             position++;
             uint32_t st, pos_state, cur_and1, match_price, rep_match_price, cur_byte, match_byte;
             // every slot the step touches is <= cur + 1: LDS only when that is below kOptLds
+#ifdef LZG_PROF
+            if (cur + 1 >= (uint32_t)kOptLds) PCOUNT(PF_NSPILL);
+#endif
             const bool next_is_char =
                 cur + 1 < (uint32_t)kOptLds
                     ? pos_step<true>(cur, position, st, pos_state, cur_and1, match_price, rep_match_price, cur_byte, match_byte)
                     : pos_step<false>(cur, position, st, pos_state, cur_and1, match_price, rep_match_price, cur_byte, match_byte);
+            if (RING && far_valid) {   // slot cur + 64 leaves the far entry for cur's, free now
+                evict_ahead(cur);
+                const uint32_t r = cur & kOptMask, e = kFarEntry;
+                const uint32_t fp = o_price[e], fpp = o_pp[e], ffs = o_fs[e];
+                const int32_t fbp = o_bp[e], fbp2 = o_bp2[e];
+                o_price[r] = fp; o_pp[r] = fpp; o_bp[r] = fbp; o_bp2[r] = fbp2; o_fs[r] = (uint8_t)ffs;
+                ring_top = cur + (uint32_t)kOptLds;
+                far_valid = 0;
+                LANE_FENCE();
+            }
             uint32_t num_avail_full = avail() + 1;
             if ((uint32_t)kNumOpts - 1 - cur < num_avail_full) num_avail_full = kNumOpts - 1 - cur;
             uint32_t num_avail = num_avail_full;
@@ -1065,8 +1190,8 @@ struct Enc {
                     uint32_t psn = (position + 1) & ps_mask;
                     uint32_t nrmp = cur_and1 + dm1(E_IS_MATCH + (st2 << PBS) + psn) + dm1(E_IS_REP + st2);
                     uint32_t offset = cur + 1 + lt2;
-                    extend_to(len_end, offset);
-                    relax_two_step(offset, nrmp + rep_price(0, lt2, st2, psn), cur + 1, false, 0, 0);
+                    extend_to(len_end, offset, cur);
+                    relax_two_step(offset, nrmp + rep_price(0, lt2, st2, psn), cur + 1, false, 0, 0, cur);
                     PEND(PF_RELAX, t2b);
                 }
             }
@@ -1080,7 +1205,7 @@ struct Enc {
                 PEND(PF_REPLEN, tr);
                 if (lt < 2) continue;
                 PBEGIN(trr);
-                extend_to(len_end, cur + lt);
+                extend_to(len_end, cur + lt, cur);
                 relax_rep(cur, 2, lt, rep_match_price + pure_rep_price(ri, st, pos_state), pos_state, cur, ri);
                 PEND(PF_RELAX, trr);
                 if (ri == 0) start_len = lt + 1;
@@ -1102,8 +1227,8 @@ struct Enc {
                         psn = (position + lt + 1) & ps_mask;
                         uint32_t nrmp = clcp + dm1(E_IS_MATCH + (st2 << PBS) + psn) + dm1(E_IS_REP + st2);
                         uint32_t offset = lt + 1 + lt2;
-                        extend_to(len_end, cur + offset);
-                        relax_two_step(cur + offset, nrmp + rep_price(0, lt2, st2, psn), cur + lt + 1, true, cur, (int32_t)ri);
+                        extend_to(len_end, cur + offset, cur);
+                        relax_two_step(cur + offset, nrmp + rep_price(0, lt2, st2, psn), cur + lt + 1, true, cur, (int32_t)ri, cur);
                         PEND(PF_TWOREL, tq2);
                     }
                 }
@@ -1121,7 +1246,7 @@ struct Enc {
                 uint64_t tm = PCLK();
 #endif
                 uint32_t normal_match_price = match_price + dm0(E_IS_REP + st);
-                extend_to(len_end, cur + new_len);
+                extend_to(len_end, cur + new_len, cur);
                 uint32_t offs = 0;
                 while (offs + 1 < npairs && start_len > md_len[offs]) offs++;
                 uint32_t seg_lo = start_len;
@@ -1155,9 +1280,9 @@ struct Enc {
                             psn = (position + lt + 1) & ps_mask;
                             uint32_t nrmp = clcp + dm1(E_IS_MATCH + (st2 << PBS) + psn) + dm1(E_IS_REP + st2);
                             uint32_t offset = lt + 1 + lt2;
-                            extend_to(len_end, cur + offset);
+                            extend_to(len_end, cur + offset, cur);
                             relax_two_step(cur + offset, nrmp + rep_price(0, lt2, st2, psn), cur + lt + 1, true, cur,
-                                           (int32_t)(cur_back + kNumRepDistances));
+                                           (int32_t)(cur_back + kNumRepDistances), cur);
                             PEND(PF_TWOREL, tm3);
                         }
                     }
@@ -1295,10 +1420,11 @@ struct Enc {
                 // The match byte was taken with the rep0 of the slot's own best path; a
                 // two-step candidate's middle literal can sit on a path with another rep0
                 // (then the byte is re-read). Slot 0 always used the current rep0.
-                const bool fs_ = sym_slot < (uint32_t)kOptLds;
-                const uint32_t b = fs_ ? bytes_at<true>(sym_slot) : bytes_at(sym_slot);
-                const uint32_t r0 = fs_ ? back_at<true>(sym_slot, 0) : back_at(sym_slot, 0);
-                prev_byte = b >> 16;
+                const uint32_t top = opt_end > 0 ? (uint32_t)opt_end - 1 : 0u;   // behind fields written: slots <= top
+                const bool fs_ = b_in(sym_slot, top);
+                const uint32_t b = fs_ ? bytes_at<true>(sym_slot, top) : bytes_at(sym_slot, top);
+                const uint32_t r0 = fs_ ? back_at<true>(sym_slot, 0, top) : back_at(sym_slot, 0, top);
+                prev_byte = (b >> 16) & 0xFFu;
                 uint32_t mb = (b >> 8) & 0xFFu;
                 if (sym_slot != 0 && r0 != rd0) mb = byte_at((int32_t)(0 - rd0 - 1) - additional_offset);
                 encode_symbol(-1, 1, now_pos, b & 0xFFu, mb, false);
@@ -1329,7 +1455,7 @@ __host__ __device__ inline uint32_t enc_lds_layout(const EncArgs& a, uint32_t* o
     const uint32_t sz[L_COUNT] = {
         512 * 2, prob_count(a.pb) * 2 + 2, dm_count(a.pb) * 4 + 4, 2 * (1u << a.pb) * a.len_table_size * 2, 2 * 16 * 4, 256 * 2, 512 * 2, 16 * 4,
         0u /* tp aliases the gather window */, md_cap * 2, md_cap * 4, kRing * 4, kRing * kInlinePairs * a.pair_bytes,
-        (kOptLds + 1) * 4, (kOptLds + 1) * 4, (kOptLds + 1) * 4, kOptLds * 4, kOptLds + 1, 4 * kOptLds * 4, kOptLds * 4, kSides * kGW, kRbuf * 2 + 2,
+        (kOptLds + 2) * 4, (kOptLds + 2) * 4, (kOptLds + 2) * 4, (kOptLds + 2) * 4, kOptLds + 2, 4 * kOptLds * 4, kOptLds * 4, kSides * kGW, kRbuf * 2 + 2,
         a.lit_in_lds ? (0x300u << (a.lc + a.lp)) * 2 + 2 : 0u};
     uint32_t o = 0;
     for (int i = 0; i < L_COUNT; i++) { if (off) off[i] = o; o += (sz[i] + 15) & ~15u; }
@@ -1337,11 +1463,12 @@ __host__ __device__ inline uint32_t enc_lds_layout(const EncArgs& a, uint32_t* o
 }
 
 // SPEC = 1: the level-5 parameters of bench.py (fb 32, lc 3, lp 0, pb 2, no end
-// marker) as compile-time constants; SPEC = 0: any parameters.
+// marker) as compile-time constants; SPEC = 2: any parameters with fb <= 32;
+// SPEC = 0: fb > 32. SPEC 1 and 2 keep _optimum in the LDS ring.
 template <typename PairT, bool LIT_LDS, int PBS, int SPEC>
 __global__ void __launch_bounds__(kWave, 4) enc_kernel(EncArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    Enc<PairT, LIT_LDS, PBS> e;
+    Enc<PairT, LIT_LDS, PBS, (SPEC != 0)> e;   // SPEC 1 and 2: fb <= 32, the _optimum ring
     e.lane = threadIdx.x;
     if (SPEC == 1) {
         e.fb = 32; e.lc = 3; e.lp = 0; e.pb = 2; e.ps_mask = 3; e.eos = 0; e.tsize = 31;
@@ -1457,7 +1584,8 @@ static void launch_one(Ctx* ctx, const EncArgs& a, int grid, size_t lds, hipStre
             return;
         }
     }
-    launch_spec<PairT, LIT, PBS, 0>(ctx, a, grid, lds, st);
+    if (a.fb <= 32) launch_spec<PairT, LIT, PBS, 2>(ctx, a, grid, lds, st);
+    else launch_spec<PairT, LIT, PBS, 0>(ctx, a, grid, lds, st);
 }
 
 template <typename PairT, bool LIT>

@@ -282,7 +282,7 @@ struct EncArgs {
 
 // encoder phase profile slots (LZG_PROF builds)
 enum { PF_TOTAL, PF_GETOPT, PF_MATCHES, PF_REPLEN, PF_TWOLEN, PF_LIT, PF_RELAX, PF_TWOREL, PF_STATE, PF_BACK,
-       PF_ENCODE, PF_TABLES, PF_NOPT, PF_NPOS, PF_T0, PF_T1, PF_HWID, kProfSlots };
+       PF_ENCODE, PF_TABLES, PF_NOPT, PF_NPOS, PF_NSPILL, PF_NOVF, PF_NTWO, PF_T0, PF_T1, PF_HWID, kProfSlots };
 
 int launch_encoder(Ctx* ctx, const EncArgs& a, bool wide_pairs, int grid, hipStream_t st);
 

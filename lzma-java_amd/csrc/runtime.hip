@@ -55,7 +55,8 @@ static void report_profile(const uint64_t* d_prof, int ns, uint64_t total, hipSt
     hipStreamSynchronize(st);
     static const char* names[kProfSlots] = {"total", "get_optimum", "match_lists", "rep_len", "two_step_len", "lit_price",
                                             "relax", "two_step_relax", "state", "backward", "encode", "tables",
-                                            "n_getopt", "n_positions", "t0", "t1", "hwid"};
+                                            "n_getopt", "n_positions", "n_spill_steps", "n_ovf_lists",
+                                            "n_two_step", "t0", "t1", "hwid"};
     double sum[kProfSlots] = {0};
     uint64_t mx = 0;
     for (int i = 0; i < ns; i++) {

@@ -24,6 +24,7 @@ static std::vector<uint8_t> make_input(int kind, size_t n, unsigned seed) {
                   while (i < n) { const char* s = w[rng() % 6]; for (size_t k = 0; s[k] && i < n; k++) v[i++] = (uint8_t)s[k]; } break; }
         case 3: for (size_t i = 0; i < n; i++) v[i] = (uint8_t)("abcdefghij"[i % 10]); break;
         case 4: lzma_bench_generate(v.data(), n); break;
+        case 6: lzma_text_generate(v.data(), n, seed); break;   // deep getOptimum parses (_optimum ring)
         default: if (n) memset(v.data(), 0, n);
     }
     return v;
@@ -50,6 +51,7 @@ int main(int argc, char** argv) {
         std::vector<std::vector<uint8_t>> ins;
         for (int kind = 0; kind < (tiny ? 2 : 6); kind++)
             for (size_t n : sizes) ins.push_back(make_input(kind, n, (unsigned)(kind * 1000 + n + pi)));
+        if (!tiny) ins.push_back(make_input(6, full ? 200000 : 40000, (unsigned)(7 + pi)));
         std::vector<uint64_t> offs(ins.size() + 1, 0);
         std::vector<uint8_t> cat;
         for (size_t i = 0; i < ins.size(); i++) { cat.insert(cat.end(), ins[i].begin(), ins[i].end()); offs[i + 1] = cat.size(); }

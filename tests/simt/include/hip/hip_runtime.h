@@ -236,6 +236,11 @@ inline unsigned atomicAdd(unsigned* p, unsigned v);
 #define __builtin_amdgcn_fence(order, scope) __atomic_signal_fence(__ATOMIC_SEQ_CST)
 // wave width 1: the first active lane is the only lane
 inline int __builtin_amdgcn_readfirstlane(int v) { return v; }
+#ifdef LZG_PROF   // the encoder's phase profile: counters only (no clock in the emulation)
+inline uint64_t __builtin_amdgcn_s_memtime() { return 0; }
+inline uint64_t __builtin_amdgcn_s_memrealtime() { return 0; }
+inline unsigned __builtin_amdgcn_s_getreg(int) { return 0; }
+#endif
 inline int __builtin_amdgcn_readlane(int v, int) { return v; }
 #define __builtin_nontemporal_load(p) (*(p))
 #define __builtin_nontemporal_store(v, p) (*(p) = (v))

@@ -1,6 +1,6 @@
 """Encoder throughput vs. number of concurrent streams (device-resident).
 
-usage: python tools/enc_scaling.py [chunk_bytes] [counts_csv]
+usage: python tools/enc_scaling.py [chunk_bytes] [counts_csv] [bench|text] [dict_log]
 With LZMA_AMD_LIB=lzma-java_amd/build/prof/liblzma_mi355x.so the library
 prints the per-phase cycle profile of each pass to stderr.
 """
@@ -19,11 +19,13 @@ import lzma_amd  # noqa: E402
 def main():
     chunk = int(sys.argv[1]) if len(sys.argv) > 1 else 256 << 10
     counts = [int(x) for x in (sys.argv[2] if len(sys.argv) > 2 else "1,64,256,1024").split(",")]
+    kind = sys.argv[3] if len(sys.argv) > 3 else "bench"
+    dict_log = int(sys.argv[4]) if len(sys.argv) > 4 else (28 if kind == "text" else 26)
     dev = torch.device("cuda", 0)
     total = chunk * max(counts)
-    host = lzma_amd.bench_generate(total)
+    host = lzma_amd.generate(kind, total)
     d_in = torch.from_numpy(host).to(dev)
-    p = lzma_amd.make_params(dict_size=1 << 26, fb=32, mf=1, lc=3, lp=0, pb=2)
+    p = lzma_amd.make_params(dict_size=1 << dict_log, fb=32, mf=1, lc=3, lp=0, pb=2)
     ctx = lzma_amd.Context(0)
     ctx.set_batch_bytes(max(total, 1 << 20))
     st = torch.cuda.current_stream(dev).cuda_stream
