@@ -322,8 +322,13 @@ __device__ inline uint32_t common_len(const uint8_t* a, const uint8_t* b, uint32
     return limit;
 }
 
+#ifdef LZG_WALK_WAVES   // experiment: a VGPR budget for more waves per SIMD (memory-level parallelism)
+#define LZG_WALK_ATTR __attribute__((amdgpu_waves_per_eu(LZG_WALK_WAVES, LZG_WALK_WAVES)))
+#else
+#define LZG_WALK_ATTR
+#endif
 template <typename PairT, bool BT4>
-__global__ void __launch_bounds__(64) mf_walk_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ offs,
+__global__ void __launch_bounds__(64) LZG_WALK_ATTR mf_walk_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ offs,
                                                      const uint64_t* __restrict__ keys4, const uint32_t* __restrict__ vals4,
                                                      const uint32_t* __restrict__ chain_order,
                                                      const uint32_t* __restrict__ chain_start,
@@ -360,9 +365,37 @@ __global__ void __launch_bounds__(64) mf_walk_kernel(const uint8_t* __restrict__
     // position ends, and the newest member's node (the next position's first
     // tree node) is carried in registers instead of being re-read.
     WNode head{};                            // node of the previous member (valid when prev_local != 0)
+    // Software pipeline over the bucket's members: the inputs of member i + 1 (its
+    // prefix, its hash2/hash3 candidates' first bytes) and the candidates of member
+    // i + 2 are loaded at the start of member i, so they arrive while member i walks
+    // the tree instead of in front of member i + 1's walk.
+    const uint32_t* __restrict__ prev2 = a.prev2;
+    const uint32_t* __restrict__ prev3 = a.prev3;
+    auto cand = [&](uint64_t gi, uint32_t& v2, uint32_t& v3) {
+        v2 = BT4 ? __builtin_nontemporal_load(prev2 + gi) : kNoPos;
+        v3 = BT4 ? __builtin_nontemporal_load(prev3 + gi) : kNoPos;
+    };
+    auto cand_bytes = [&](uint32_t v2, uint32_t v3, uint32_t& b2, uint32_t& b3) {
+        b2 = BT4 && v2 != kNoPos ? (uint32_t)in[v2] : 0u;   // first byte of the candidate (batch-global index)
+        b3 = BT4 && v3 != kNoPos ? (uint32_t)in[v3] : 0u;
+    };
     uint64_t g = vals4[start];
+    uint64_t g1 = start + 1 < end ? vals4[start + 1] : 0, g2 = start + 2 < end ? vals4[start + 2] : 0;
+    uint32_t pv2, pv3, pv2n = kNoPos, pv3n = kNoPos, b2, b3;
+    cand(g, pv2, pv3);
+    if (start + 1 < end) cand(g1, pv2n, pv3n);
+    uint64_t c0 = load8(sb + (g - base)), c1 = load8(sb + (g - base) + 8);   // this member's prefix
+    cand_bytes(pv2, pv3, b2, b3);
     for (uint64_t i = start; i < end; i++) {
-        const uint64_t g_next = i + 1 < end ? vals4[i + 1] : 0;
+        const uint64_t g3 = i + 3 < end ? vals4[i + 3] : 0;
+        uint32_t pv2nn = kNoPos, pv3nn = kNoPos, b2n = 0, b3n = 0;
+        uint64_t c0n = 0, c1n = 0;
+        if (i + 2 < end) cand(g2, pv2nn, pv3nn);
+        if (i + 1 < end) {
+            c0n = load8(sb + (g1 - base));
+            c1n = load8(sb + (g1 - base) + 8);
+            cand_bytes(pv2n, pv3n, b2n, b3n);
+        }
         uint32_t p = (uint32_t)(g - base);
         uint32_t pos = p + 1;               // BinTree 1-based position
         uint64_t rem = n - p;
@@ -397,15 +430,13 @@ __global__ void __launch_bounds__(64) mf_walk_kernel(const uint8_t* __restrict__
             last_d = d;
             cnt++;
         };
-        const uint64_t c0 = load8(cur), c1 = load8(cur + 8);   // this member's prefix
         const uint32_t cur0 = (uint32_t)(c0 & 0xFFu);
         if (BT4) {   // hash2 / hash3 candidates, BinTree.java:183-207
-            uint32_t pv2 = __builtin_nontemporal_load(a.prev2 + g), pv3 = __builtin_nontemporal_load(a.prev3 + g);
             uint32_t cm2 = pv2 == kNoPos ? 0 : (uint32_t)(pv2 - base) + 1;
             uint32_t cm3 = pv3 == kNoPos ? 0 : (uint32_t)(pv3 - base) + 1;
-            if (cm2 > match_min && sb[cm2 - 1] == cur0) { max_len = 2; emit(2, pos - cm2 - 1); }
+            if (cm2 > match_min && b2 == cur0) { max_len = 2; emit(2, pos - cm2 - 1); }
             const uint32_t d2 = pos - cm2 - 1;   // the len-2 pair's distance, if it was emitted
-            if (cm3 > match_min && sb[cm3 - 1] == cur0) {
+            if (cm3 > match_min && b3 == cur0) {
                 if (cm3 == cm2) cnt--;
                 max_len = 3;
                 emit(3, pos - cm3 - 1);
@@ -486,7 +517,10 @@ __global__ void __launch_bounds__(64) mf_walk_kernel(const uint8_t* __restrict__
         // outputs are touched once: non-temporal, so the stream's nodes and bytes keep the L2
         store_rec<PairT>(recs + g * rec_vecs<PairT>(), q0, q1, q2, q3, cnt | (ml << 16));
         prev_local = pos;
-        g = g_next;
+        g = g1; g1 = g2; g2 = g3;
+        c0 = c0n; c1 = c1n;
+        pv2 = pv2n; pv3 = pv3n; pv2n = pv2nn; pv3n = pv3nn;
+        b2 = b2n; b3 = b3n;
     }
 }
 
