@@ -22,6 +22,8 @@
 #include "lzma_common.h"
 #include "runtime.h"
 
+#include <cstdio>
+
 namespace lzg {
 
 static __constant__ Tables c_tab = make_tables();
@@ -151,6 +153,16 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* wsum) 
     return before + x - v;
 }
 
+// Long chains first, across all streams. A bucket's walk is serial, so a long
+// one is the walk's tail: in stream order, the long buckets of the last streams
+// start when their stream's turn comes and finish long after the short ones.
+// Chains of kWalkLong or more members are therefore walked by the blocks at the
+// front of the grid, longest length class (floor(log2 len)) first, beside the
+// stream-ordered short ones (TEXT walk 929 -> 757 ms, BENCH 138 -> 132 ms). Order
+// within a class is free: a chain's walk touches only its own positions, nodes
+// and records. mf_chains_kernel lists them (unordered) and counts the classes.
+constexpr uint32_t kWalkLong = 256;
+
 // Walk-order key of a chain: longest first (lanes of one wave walk similar-length
 // buckets); exact below 128, then 8 steps per doubling. Only the order depends on it.
 __device__ __forceinline__ uint32_t chain_order_key(uint32_t len) {
@@ -172,7 +184,8 @@ constexpr uint32_t kChainThreads = 256, kChainItems = 4;
 __global__ void __launch_bounds__(kChainThreads) mf_chains_kernel(const uint64_t* __restrict__ offs, const uint64_t* __restrict__ keys,
                                                                    uint32_t* __restrict__ chain_start, uint32_t* __restrict__ chain_len,
                                                                    uint32_t* __restrict__ okey, uint32_t* __restrict__ cidx,
-                                                                   uint64_t* __restrict__ seg_end) {
+                                                                   uint64_t* __restrict__ seg_end, uint32_t long_min,
+                                                                   uint32_t* __restrict__ cls, uint32_t* __restrict__ long_raw) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];   // dynamic LDS (the CPU emulation shares it)
     uint32_t* wsum = (uint32_t*)smem;                                   // [kChainThreads / 64]
     uint32_t* tile_tot = wsum + kChainThreads / 64;                     // [2]: heads, valid items
@@ -215,6 +228,10 @@ __global__ void __launch_bounds__(kChainThreads) mf_chains_kernel(const uint64_t
         chain_len[lo + c] = len;
         okey[lo + c] = chain_order_key(len);
         cidx[lo + c] = (uint32_t)(lo + c);
+        if (len >= long_min) {
+            long_raw[atomicAdd(&cls[64], 1u)] = (uint32_t)(lo + c);
+            atomicAdd(&cls[31 - __clz((int)len)], 1u);
+        }
     }
     if (tid == 0) seg_end[s] = lo + nch;
 }
@@ -322,6 +339,22 @@ __device__ inline uint32_t common_len(const uint8_t* a, const uint8_t* b, uint32
     return limit;
 }
 
+// scatter cursors of the long chains: the classes laid out longest first (one thread)
+__global__ void mf_long_offsets_kernel(uint32_t* __restrict__ cls) {
+    if (threadIdx.x != 0) return;
+    uint32_t off = 0;
+    for (int k = 31; k >= 0; k--) { cls[32 + k] = off; off += cls[k]; }
+}
+// the long chains in class order (longest class first)
+__global__ void __launch_bounds__(256) mf_long_scatter_kernel(const uint32_t* __restrict__ long_raw, uint32_t n_long,
+                                                              const uint32_t* __restrict__ chain_len, uint32_t* __restrict__ cls,
+                                                              uint32_t* __restrict__ long_list) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_long) return;
+    const uint32_t c = long_raw[i];
+    long_list[atomicAdd(&cls[32 + 31 - __clz((int)chain_len[c])], 1u)] = c;
+}
+
 #ifdef LZG_WALK_WAVES   // experiment: a VGPR budget for more waves per SIMD (memory-level parallelism)
 #define LZG_WALK_ATTR __attribute__((amdgpu_waves_per_eu(LZG_WALK_WAVES, LZG_WALK_WAVES)))
 #else
@@ -334,21 +367,34 @@ __global__ void __launch_bounds__(64) LZG_WALK_ATTR mf_walk_kernel(const uint8_t
                                                      const uint32_t* __restrict__ chain_start,
                                                      const uint32_t* __restrict__ chain_len,
                                                      uint64_t nchains,
+                                                     const uint32_t* __restrict__ long_list, uint64_t n_long,
+                                                     uint32_t long_blocks, uint32_t min_len,
                                                      MfArgs a, WNode* __restrict__ nodes, v4u32* __restrict__ recs,
                                                      uint32_t* __restrict__ ovf_off, PairT* __restrict__ ovf,
                                                      unsigned long long* __restrict__ ovf_used, uint64_t ovf_cap,
                                                      uint32_t ovf_stride,
                                                      int* __restrict__ err) {
     using PP = PairPack<PairT>;
-    // XCD-aware mapping: the dispatcher places block b on XCD b % 8, so XCD x takes
-    // the x-th eighth of the (stream-ordered) chain list and its L2 serves a few streams
-    const uint32_t per_xcd = gridDim.x / 8;   // the host pads the grid to a multiple of 8
-    const uint64_t blk = (uint64_t)(blockIdx.x % 8) * per_xcd + blockIdx.x / 8;
-    uint64_t ci = blk * blockDim.x + threadIdx.x;
-    if (ci >= nchains) return;
-    uint32_t c = chain_order[ci];
+    uint32_t c;
+    if (blockIdx.x < long_blocks) {   // the long chains, longest first, dealt over the XCDs in dispatch order
+        const uint64_t li = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+        if (li >= n_long) return;
+        c = long_list[li];
+    } else {
+        // XCD-aware mapping: the dispatcher places block b on XCD b % 8, so XCD x takes
+        // the x-th eighth of the (stream-ordered) chain list and its L2 serves a few
+        // streams (long_blocks and the grid are multiples of 8: b keeps its XCD)
+        const uint32_t b = blockIdx.x - long_blocks;
+        const uint32_t per_xcd = (gridDim.x - long_blocks) / 8;
+        const uint64_t blk = (uint64_t)(b % 8) * per_xcd + b / 8;
+        const uint64_t ci = blk * blockDim.x + threadIdx.x;
+        if (ci >= nchains) return;
+        c = chain_order[ci];
+        if (chain_len[c] >= min_len) return;   // walked by the front blocks
+    }
     uint64_t start = chain_start[c], end = start + chain_len[c];
     if (start == end) return;   // a stream's sentinel run
+    if (end - start < a.walk_lo || end - start > a.walk_hi) return;   // timing experiment only (LZG_WALK_ONLY)
     uint64_t key = keys4[start];
     int s = (int)(key >> (BT4 ? a.hash_bits : 16));
     uint64_t base = offs[s], n = offs[s + 1] - base;
@@ -543,6 +589,11 @@ int run_match_finder(Ctx* ctx, const Derived& d, const uint8_t* in, const uint64
     MfArgs a{};
     a.fb = d.fb; a.min_match_check = d.min_match_check; a.hash_mask = d.hash_mask; a.hash_bits = d.hash_bits;
     a.cut_value = d.cut_value; a.cyc_size = d.cyc_size; a.direct_bytes = d.direct_bytes;
+    a.walk_lo = 0; a.walk_hi = 0xFFFFFFFFu;
+    if (const char* e = getenv("LZG_WALK_ONLY")) {   // "lo,hi": a timing experiment; the output is incomplete
+        unsigned lo = 0, hi = 0xFFFFFFFFu;
+        if (sscanf(e, "%u,%u", &lo, &hi) >= 1) { a.walk_lo = lo; a.walk_hi = hi; }
+    }
     a.k4 = w.k4; a.k3 = (uint32_t*)w.k3; a.k2 = (uint32_t*)w.k2; a.vals = w.vals; a.mrec = w.pairs; a.rec_vecs = wide_pairs ? rec_vecs<uint64_t>() : rec_vecs<uint32_t>(); a.prev2 = w.prev2; a.prev3 = w.prev3;
     const bool bt4 = d.hash_array != 0;
     const unsigned B = 256;
@@ -576,36 +627,49 @@ int run_match_finder(Ctx* ctx, const Derived& d, const uint8_t* in, const uint64
     // arrays are dead here and hold the order keys.
     uint32_t* okey = (uint32_t*)w.k2;
     uint32_t* okey_sorted = (uint32_t*)w.k3;
+    uint32_t* long_raw = (uint32_t*)w.k4;   // dead since the hash4 sort
+    // LZG_WALK_LONG overrides the long-chain threshold (experiments; 4294967295 = stream order only)
+    static const uint32_t long_min = getenv("LZG_WALK_LONG") ? (uint32_t)strtoul(getenv("LZG_WALK_LONG"), nullptr, 10) : kWalkLong;
     {
         TimedLaunch tl(ctx, "mf_sort", st);
+        hipMemsetAsync(w.cls, 0, 96 * sizeof(uint32_t), st);
         hipLaunchKernelGGL(mf_chains_kernel, dim3(nstreams), dim3(kChainThreads), (kChainThreads / 64 + 2) * 4, st, d_offs, w.ks,
-                           w.chain_start, w.chain_len, okey, w.chain_idx, w.seg_end);
+                           w.chain_start, w.chain_len, okey, w.chain_idx, w.seg_end, long_min, w.cls, long_raw);
         hipLaunchKernelGGL(mf_chain_scan_kernel, dim3(1), dim3(kChainThreads), (kChainThreads / 64 + 2) * 4, st, d_offs, w.seg_end,
                            nstreams, w.chain_offs);
         if ((rc = seg_radix_sort(ctx, false, okey, w.chain_idx, okey_sorted, w.chain_order, w.son, w.son + total, w.hist, total,
                                  d_offs, nstreams, 8, st, w.seg_end, w.chain_offs))) return rc;
     }
     uint64_t nchains = 0;   // sizes the walk grid: one host round trip per pass
+    uint32_t n_long = 0;    // the long chains (walked first)
     if (hipMemcpyAsync(&nchains, w.chain_offs + nstreams, sizeof(nchains), hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipMemcpyAsync(&n_long, w.cls + 64, sizeof(n_long), hipMemcpyDeviceToHost, st) != hipSuccess ||
         hipStreamSynchronize(st) != hipSuccess)
         return ctx->fail(LZMA_E_DEVICE, "mf: chain count: %s", hipGetErrorString(hipGetLastError()));
     LZG_TRACE(ctx, st, "mf sorts + chain lists done");
     if (nchains == 0) return LZMA_OK;
+    if (n_long) {
+        TimedLaunch tl(ctx, "mf_sort", st);
+        hipLaunchKernelGGL(mf_long_offsets_kernel, dim3(1), dim3(64), 0, st, w.cls);
+        hipLaunchKernelGGL(mf_long_scatter_kernel, dim3((n_long + B - 1) / B), dim3(B), 0, st, long_raw, n_long, w.chain_len, w.cls,
+                           w.long_list);
+    }
     hipMemsetAsync(w.ovf_used, 0, sizeof(unsigned long long), st);
     hipMemsetAsync(w.err, 0, sizeof(int), st);
     {
         TimedLaunch tl(ctx, "mf_walk", st);
         const unsigned WB = 64;
+        const unsigned long_blocks = (unsigned)(((n_long + WB - 1) / WB + 7) & ~7ull);
         unsigned grid = (unsigned)((nchains + WB - 1) / WB);
-        grid = (grid + 7) & ~7u;   // multiple of 8 (XCD-aware mapping in mf_walk_kernel)
+        grid = ((grid + 7) & ~7u) + long_blocks;   // multiples of 8 (XCD-aware mapping in mf_walk_kernel)
         // experiment: dynamic LDS per wave caps the waves per CU (L2 working set)
         static const size_t walk_lds = getenv("LZG_WALK_LDS") ? (size_t)atoi(getenv("LZG_WALK_LDS")) : 0;
         if (wide_pairs) {
-            if (bt4) hipLaunchKernelGGL((mf_walk_kernel<uint64_t, true>), dim3(grid), dim3(WB), walk_lds, st, in, d_offs, w.ks, w.vs, w.chain_order, w.chain_start, w.chain_len, nchains, a, (WNode*)w.son, w.pairs, w.ovf_off, (uint64_t*)w.ovf, w.ovf_used, w.ovf_cap, ovf_stride(d.fb), w.err);
-            else hipLaunchKernelGGL((mf_walk_kernel<uint64_t, false>), dim3(grid), dim3(WB), walk_lds, st, in, d_offs, w.ks, w.vs, w.chain_order, w.chain_start, w.chain_len, nchains, a, (WNode*)w.son, w.pairs, w.ovf_off, (uint64_t*)w.ovf, w.ovf_used, w.ovf_cap, ovf_stride(d.fb), w.err);
+            if (bt4) hipLaunchKernelGGL((mf_walk_kernel<uint64_t, true>), dim3(grid), dim3(WB), walk_lds, st, in, d_offs, w.ks, w.vs, w.chain_order, w.chain_start, w.chain_len, nchains, w.long_list, (uint64_t)n_long, long_blocks, long_min, a, (WNode*)w.son, w.pairs, w.ovf_off, (uint64_t*)w.ovf, w.ovf_used, w.ovf_cap, ovf_stride(d.fb), w.err);
+            else hipLaunchKernelGGL((mf_walk_kernel<uint64_t, false>), dim3(grid), dim3(WB), walk_lds, st, in, d_offs, w.ks, w.vs, w.chain_order, w.chain_start, w.chain_len, nchains, w.long_list, (uint64_t)n_long, long_blocks, long_min, a, (WNode*)w.son, w.pairs, w.ovf_off, (uint64_t*)w.ovf, w.ovf_used, w.ovf_cap, ovf_stride(d.fb), w.err);
         } else {
-            if (bt4) hipLaunchKernelGGL((mf_walk_kernel<uint32_t, true>), dim3(grid), dim3(WB), walk_lds, st, in, d_offs, w.ks, w.vs, w.chain_order, w.chain_start, w.chain_len, nchains, a, (WNode*)w.son, w.pairs, w.ovf_off, (uint32_t*)w.ovf, w.ovf_used, w.ovf_cap, ovf_stride(d.fb), w.err);
-            else hipLaunchKernelGGL((mf_walk_kernel<uint32_t, false>), dim3(grid), dim3(WB), walk_lds, st, in, d_offs, w.ks, w.vs, w.chain_order, w.chain_start, w.chain_len, nchains, a, (WNode*)w.son, w.pairs, w.ovf_off, (uint32_t*)w.ovf, w.ovf_used, w.ovf_cap, ovf_stride(d.fb), w.err);
+            if (bt4) hipLaunchKernelGGL((mf_walk_kernel<uint32_t, true>), dim3(grid), dim3(WB), walk_lds, st, in, d_offs, w.ks, w.vs, w.chain_order, w.chain_start, w.chain_len, nchains, w.long_list, (uint64_t)n_long, long_blocks, long_min, a, (WNode*)w.son, w.pairs, w.ovf_off, (uint32_t*)w.ovf, w.ovf_used, w.ovf_cap, ovf_stride(d.fb), w.err);
+            else hipLaunchKernelGGL((mf_walk_kernel<uint32_t, false>), dim3(grid), dim3(WB), walk_lds, st, in, d_offs, w.ks, w.vs, w.chain_order, w.chain_start, w.chain_len, nchains, w.long_list, (uint64_t)n_long, long_blocks, long_min, a, (WNode*)w.son, w.pairs, w.ovf_off, (uint32_t*)w.ovf, w.ovf_used, w.ovf_cap, ovf_stride(d.fb), w.err);
         }
     }
     LZG_TRACE(ctx, st, "mf_walk done (%llu chains)", (unsigned long long)nchains);

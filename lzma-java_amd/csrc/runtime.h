@@ -29,14 +29,15 @@ struct MfArgs {
     uint32_t *k3, *k2;            // (stream << 16 | hash3), (stream << 10 | hash2): < 2^30 for <= 16384 streams
     uint32_t *vals, *prev2, *prev3;
     v4u32* mrec;                  // per-position match-list records (lzma_common.h store_rec)
+    uint32_t walk_lo, walk_hi;    // experiment hook (LZG_WALK_ONLY): walk only chains of length in [lo, hi]
 };
 
 struct MfBuffers {
     uint64_t *k4, *k3, *k2, *ks;
     uint32_t *vals, *vs, *prev2, *prev3;
     uint8_t* flag;
-    uint32_t *chain_start, *chain_len, *chain_len_sorted, *chain_idx, *chain_order;
-    uint64_t* counts;
+    uint32_t *chain_start, *chain_len, *long_list, *chain_idx, *chain_order;
+    uint32_t* cls;                // long chains per length class [32], the scatter cursors [32], the long count [1]
     uint64_t* son;                // walk tree nodes (mf.hip WNode, 32 B per position: links + 16-byte prefix);
                                   // before the walk, the sorts' ping-pong buffers
     uint32_t* hist;               // sort.hip digit histograms, [nstreams][4][256]

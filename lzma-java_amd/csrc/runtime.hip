@@ -141,9 +141,9 @@ static int encode_pass(Ctx* ctx, const Derived& d, const uint8_t* d_in, const ui
             w.vals = c.take<uint32_t>(T); w.vs = c.take<uint32_t>(T);
             w.prev2 = c.take<uint32_t>(T); w.prev3 = c.take<uint32_t>(T);
             w.flag = c.take<uint8_t>(T);
-            w.chain_start = c.take<uint32_t>(T); w.chain_len = c.take<uint32_t>(T); w.chain_len_sorted = c.take<uint32_t>(T);
+            w.chain_start = c.take<uint32_t>(T); w.chain_len = c.take<uint32_t>(T); w.long_list = c.take<uint32_t>(T);
             w.chain_idx = c.take<uint32_t>(T); w.chain_order = c.take<uint32_t>(T);
-            w.counts = c.take<uint64_t>(2);
+            w.cls = c.take<uint32_t>(96);
             w.son = c.take<uint64_t>(4 * T);   // mf.hip WNode: 32 bytes per position
             w.hist = c.take<uint32_t>((size_t)ns * 1024);
             w.seg_end = c.take<uint64_t>((size_t)ns + 1);
