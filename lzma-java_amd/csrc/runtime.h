@@ -104,6 +104,15 @@ struct Ctx {
     uint8_t* tmp = nullptr;     // cub temp storage
     size_t tmp_size = 0;
     uint64_t ovf_hint = 0;      // overflow pool slots per 1024 input bytes (0 = default; grows on retry)
+    // asynchronous batch decode (lzma_dec_batch_dev_async / _wait): the per-stream
+    // lengths and verdicts land in pinned host memory, `dec_done` marks the end
+    uint64_t* dec_host = nullptr;    // pinned: offsets/sizes staging, then lens (n) + status (n / 2 words)
+    size_t dec_host_words = 0;
+    int dec_pending = 0;             // streams of the decode in flight (0 = none)
+    hipEvent_t dec_done = nullptr;
+    // parse fence (lzma_ctx_set_parse_fence): an encode pass waits for this
+    // context's decode in flight before it launches its parser
+    const Ctx* fence = nullptr;
     // timing
     bool timing = false;
     struct Pending { std::string name; hipEvent_t a, b; };

@@ -103,6 +103,7 @@ struct MatchDump {
 static int encode_pass(Ctx* ctx, const Derived& d, const uint8_t* d_in, const uint64_t* h_offs, int s0, int s1,
                        uint8_t* d_out, const uint64_t* h_out_offs, uint64_t* h_out_lens, int32_t* h_status,
                        hipStream_t st, MatchDump* dump = nullptr) {
+    if (ctx->dec_pending) return ctx->fail(LZMA_E_PARAM, "an asynchronous decode is in flight: lzma_dec_batch_dev_wait first");
     const int ns = s1 - s0;
     const uint64_t in0 = h_offs[s0];
     const uint64_t total = h_offs[s1] - in0;
@@ -254,6 +255,9 @@ static int encode_pass(Ctx* ctx, const Derived& d, const uint8_t* d_in, const ui
         HIPCHK(hipMemsetAsync(d_prof, 0, (size_t)ns * kProfSlots * 8, st));
         a.prof = d_prof;
 #endif
+        // a pipelined caller's decoder (another context) may still hold CUs: the
+        // parser needs every stream resident from its start, so it waits for it
+        if (ctx->fence && ctx->fence->dec_pending) HIPCHK(hipStreamWaitEvent(st, ctx->fence->dec_done, 0));
         if ((rc = launch_encoder(ctx, a, wide, grid, st))) return rc;
         LZG_TRACE(ctx, st, "enc_parse done");
         watch.stop();
@@ -306,12 +310,14 @@ static int encode_batch_dev(Ctx* ctx, const lzma_params* p, const uint8_t* d_in,
     return LZMA_OK;
 }
 
-static int decode_batch_dev(Ctx* ctx, const uint8_t props[5], const uint8_t* d_in, const uint64_t* h_in_offs, int nstreams,
-                            const int64_t* h_out_sizes, uint8_t* d_out, const uint64_t* h_out_offs, uint64_t* h_out_lens,
-                            int32_t* h_status, hipStream_t st) {
+// Enqueues one batch decode on st. h_* arrays are read before the first copy
+// completes only when `pinned` is false (the copies are then staged by the
+// runtime); lens/status land in h_out_lens / h_status once st reaches them.
+static int decode_enqueue(Ctx* ctx, const uint8_t props[5], const uint8_t* d_in, const uint64_t* h_in_offs, int nstreams,
+                          const int64_t* h_out_sizes, uint8_t* d_out, const uint64_t* h_out_offs, uint64_t* h_out_lens,
+                          int32_t* h_status, uint32_t* h_order, hipStream_t st) {
     lzma_params p;
     if (lzma_read_props(props, &p) != LZMA_OK) return ctx->fail(LZMA_E_PARAM, "bad properties (Decoder.SetDecoderProperties false)");
-    if (nstreams <= 0) return nstreams == 0 ? LZMA_OK : ctx->fail(LZMA_E_PARAM, "nstreams < 0");
     for (int i = 0; i < nstreams; i++) {   // the decoder kernel keeps 32-bit input positions
         if (h_in_offs[i + 1] < h_in_offs[i] || h_in_offs[i + 1] - h_in_offs[i] >= 0xFFFFFFFFull)
             return ctx->fail(LZMA_E_PARAM, "compressed stream %d: bad offsets or >= 4 GiB", i);
@@ -321,9 +327,8 @@ static int decode_batch_dev(Ctx* ctx, const uint8_t props[5], const uint8_t* d_i
     uint32_t dict = (uint32_t)props[1] | ((uint32_t)props[2] << 8) | ((uint32_t)props[3] << 16) | ((uint32_t)props[4] << 24);
     const uint32_t lc = (uint32_t)p.lc, lp = (uint32_t)p.lp, pb = (uint32_t)p.pb;
     const uint32_t lit_lds = 0;   // literal coders always in the per-stream HBM scratch (dec.hip)
-    std::vector<uint32_t> order(nstreams);
-    std::iota(order.begin(), order.end(), 0u);
-    std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
+    for (int i = 0; i < nstreams; i++) h_order[i] = (uint32_t)i;
+    std::stable_sort(h_order, h_order + nstreams, [&](uint32_t a, uint32_t b) {
         return (h_out_offs[a + 1] - h_out_offs[a]) > (h_out_offs[b + 1] - h_out_offs[b]);
     });
     const int grid = dec_grid(lc, lp, lit_lds, nstreams);
@@ -346,7 +351,7 @@ static int decode_batch_dev(Ctx* ctx, const uint8_t props[5], const uint8_t* d_i
     HIPCHK(hipMemcpyAsync(d_in_offs, h_in_offs, (nstreams + 1) * 8, hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(d_sizes, h_out_sizes, nstreams * 8, hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(d_oofs, h_out_offs, (nstreams + 1) * 8, hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(d_order, order.data(), nstreams * 4, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(d_order, h_order, nstreams * 4, hipMemcpyHostToDevice, st));
     HIPCHK(hipMemsetAsync(d_next, 0, 16, st));
     DecArgs a{};
     a.in = d_in; a.in_offs = d_in_offs; a.out_sizes = d_sizes; a.out = d_out; a.out_offs = d_oofs;
@@ -358,7 +363,66 @@ static int decode_batch_dev(Ctx* ctx, const uint8_t props[5], const uint8_t* d_i
     if (rc) return rc;
     HIPCHK(hipMemcpyAsync(h_out_lens, d_lens, nstreams * 8, hipMemcpyDeviceToHost, st));
     HIPCHK(hipMemcpyAsync(h_status, d_status, nstreams * 4, hipMemcpyDeviceToHost, st));
+    return LZMA_OK;
+}
+
+static int decode_batch_dev(Ctx* ctx, const uint8_t props[5], const uint8_t* d_in, const uint64_t* h_in_offs, int nstreams,
+                            const int64_t* h_out_sizes, uint8_t* d_out, const uint64_t* h_out_offs, uint64_t* h_out_lens,
+                            int32_t* h_status, hipStream_t st) {
+    if (ctx->dec_pending) return ctx->fail(LZMA_E_PARAM, "an asynchronous decode is in flight: lzma_dec_batch_dev_wait first");
+    if (nstreams <= 0) return nstreams == 0 ? LZMA_OK : ctx->fail(LZMA_E_PARAM, "nstreams < 0");
+    std::vector<uint32_t> order(nstreams);
+    int rc = decode_enqueue(ctx, props, d_in, h_in_offs, nstreams, h_out_sizes, d_out, h_out_offs, h_out_lens, h_status,
+                            order.data(), st);
+    if (rc) return rc;
     HIPCHK(hipStreamSynchronize(st));
+    return LZMA_OK;
+}
+
+// The asynchronous form: every host array is staged in the context's pinned
+// buffer first, so the call returns as soon as the work is enqueued.
+static int decode_batch_dev_async(Ctx* ctx, const uint8_t props[5], const uint8_t* d_in, const uint64_t* h_in_offs,
+                                  int nstreams, const int64_t* h_out_sizes, uint8_t* d_out, const uint64_t* h_out_offs,
+                                  hipStream_t st) {
+    if (ctx->dec_pending) return ctx->fail(LZMA_E_PARAM, "an asynchronous decode is already in flight on this context");
+    if (nstreams <= 0) return nstreams == 0 ? LZMA_OK : ctx->fail(LZMA_E_PARAM, "nstreams < 0");
+    const size_t n = (size_t)nstreams;
+    const size_t words = (n + 1) * 3 + n + (n + 1) / 2 * 2 + 2;   // in_offs, sizes, out_offs, lens, order + status
+    if (words > ctx->dec_host_words) {
+        if (ctx->dec_host) hipHostFree(ctx->dec_host);
+        ctx->dec_host = nullptr;
+        ctx->dec_host_words = 0;
+        if (hipHostMalloc((void**)&ctx->dec_host, words * 8, hipHostMallocDefault) != hipSuccess)
+            return ctx->fail(LZMA_E_NOMEM, "pinned decode staging");
+        ctx->dec_host_words = words;
+    }
+    if (!ctx->dec_done && hipEventCreateWithFlags(&ctx->dec_done, hipEventDisableTiming) != hipSuccess)
+        return ctx->fail(LZMA_E_DEVICE, "decode event");
+    uint64_t* in_offs = ctx->dec_host;
+    int64_t* sizes = (int64_t*)(in_offs + n + 1);
+    uint64_t* out_offs = (uint64_t*)(sizes + n + 1);
+    uint64_t* lens = out_offs + n + 1;
+    uint32_t* order = (uint32_t*)(lens + n);
+    int32_t* status = (int32_t*)(order + (n + 1) / 2 * 2);
+    memcpy(in_offs, h_in_offs, (n + 1) * 8);
+    memcpy(sizes, h_out_sizes, n * 8);
+    memcpy(out_offs, h_out_offs, (n + 1) * 8);
+    int rc = decode_enqueue(ctx, props, d_in, in_offs, nstreams, sizes, d_out, out_offs, lens, status, order, st);
+    if (rc) return rc;
+    HIPCHK(hipEventRecord(ctx->dec_done, st));
+    ctx->dec_pending = nstreams;
+    return LZMA_OK;
+}
+
+static int decode_batch_dev_wait(Ctx* ctx, uint64_t* h_out_lens, int32_t* h_status) {
+    if (!ctx->dec_pending) return LZMA_OK;
+    const size_t n = (size_t)ctx->dec_pending;
+    ctx->dec_pending = 0;
+    HIPCHK(hipEventSynchronize(ctx->dec_done));
+    const uint64_t* lens = ctx->dec_host + (n + 1) * 3;
+    const int32_t* status = (const int32_t*)((const uint32_t*)(lens + n) + (n + 1) / 2 * 2);
+    if (h_out_lens) memcpy(h_out_lens, lens, n * 8);
+    if (h_status) memcpy(h_status, status, n * 4);
     return LZMA_OK;
 }
 
@@ -433,6 +497,9 @@ void lzma_ctx_destroy(lzma_ctx* ctx) {
     hipSetDevice(ctx->device);
     ctx->resolve_timings();
     for (auto e : ctx->free_events) hipEventDestroy(e);
+    if (ctx->dec_pending) hipEventSynchronize(ctx->dec_done);
+    if (ctx->dec_done) hipEventDestroy(ctx->dec_done);
+    if (ctx->dec_host) hipHostFree(ctx->dec_host);
     if (ctx->arena) hipFree(ctx->arena);
     if (ctx->litbuf) hipFree(ctx->litbuf);
     if (ctx->tmp) hipFree(ctx->tmp);
@@ -629,6 +696,29 @@ int lzma_dec_batch_dev(lzma_ctx* ctx, const uint8_t props[5], const uint8_t* d_i
     hipSetDevice(ctx->device);
     return decode_batch_dev(ctx, props, d_in, h_in_offs, nstreams, h_out_sizes, d_out, h_out_offs, h_out_lens, h_status,
                             (hipStream_t)hip_stream);
+}
+
+int lzma_dec_batch_dev_async(lzma_ctx* ctx, const uint8_t props[5], const uint8_t* d_in, const uint64_t* h_in_offs,
+                             int nstreams, const int64_t* h_out_sizes, uint8_t* d_out, const uint64_t* h_out_offs,
+                             void* hip_stream) {
+    if (!ok_ctx(ctx) || !props || !h_in_offs || !h_out_sizes || !h_out_offs) return LZMA_E_PARAM;
+    if (check_device(ctx)) return LZMA_E_NODEVICE;
+    hipSetDevice(ctx->device);
+    return decode_batch_dev_async(ctx, props, d_in, h_in_offs, nstreams, h_out_sizes, d_out, h_out_offs,
+                                  (hipStream_t)hip_stream);
+}
+
+int lzma_dec_batch_dev_wait(lzma_ctx* ctx, uint64_t* h_out_lens, int32_t* h_status) {
+    if (!ok_ctx(ctx)) return LZMA_E_PARAM;
+    hipSetDevice(ctx->device);
+    return decode_batch_dev_wait(ctx, h_out_lens, h_status);
+}
+
+int lzma_ctx_set_parse_fence(lzma_ctx* ctx, const lzma_ctx* dec_ctx) {
+    if (!ok_ctx(ctx) || (dec_ctx && !ok_ctx(dec_ctx)) || dec_ctx == ctx) return LZMA_E_PARAM;
+    if (dec_ctx && dec_ctx->device != ctx->device) return ctx->fail(LZMA_E_PARAM, "parse fence on another device");
+    ctx->fence = dec_ctx;
+    return LZMA_OK;
 }
 
 int lzma_dec_batch(lzma_ctx* ctx, const uint8_t props[5], const uint8_t* in, const uint64_t* in_offs, int nstreams,

@@ -44,7 +44,7 @@ EXPORTED_SYMBOLS = [
     "lzma_rnd_generate", "lzma_text_generate", "lzma_match_lists",
     "lzma_mctx_create", "lzma_mctx_destroy", "lzma_mctx_last_error", "lzma_mctx_devices",
     "lzma_enc_batch_multi", "lzma_dec_batch_multi", "lzma_mctx_set_batch_bytes", "lzma_mctx_set_timing",
-    "lzma_visible_on_error",
+    "lzma_visible_on_error", "lzma_dec_batch_dev_async", "lzma_dec_batch_dev_wait", "lzma_ctx_set_parse_fence",
 ]
 
 
@@ -105,6 +105,9 @@ def lib():
         L.lzma_encode.argtypes = [vp, P, vp, u64, vp, u64, ctypes.POINTER(u64)]
         L.lzma_dec_batch_dev.argtypes = [vp, vp, vp, vp, i32, vp, vp, vp, vp, vp, vp]
         L.lzma_dec_batch.argtypes = [vp, vp, vp, vp, i32, vp, vp, vp, vp, vp]
+        L.lzma_dec_batch_dev_async.argtypes = [vp, vp, vp, vp, i32, vp, vp, vp, vp]
+        L.lzma_dec_batch_dev_wait.argtypes = [vp, vp, vp]
+        L.lzma_ctx_set_parse_fence.argtypes = [vp, vp]
         L.lzma_decode.argtypes = [vp, vp, vp, u64, ctypes.c_int64, vp, u64, ctypes.POINTER(u64)]
         L.lzma_bench_generate.argtypes = [vp, u64]
         L.lzma_bench_generate.restype = None
@@ -343,6 +346,31 @@ class Context:
                                             n, sizes.ctypes.data, _dptr(d_out), out_offs.ctypes.data,
                                             lens.ctypes.data, status.ctypes.data, ctypes.c_void_p(stream_ptr)))
         return lens[:n], status[:n]
+
+    def decode_batch_dev_async(self, props: bytes, d_in, in_offs: np.ndarray, out_sizes: np.ndarray, d_out,
+                               out_offs: np.ndarray, stream_ptr: int = 0) -> None:
+        """Enqueue a batch decode and return at once; decode_batch_dev_wait() gives (lens, status)."""
+        n = len(in_offs) - 1
+        in_offs = np.ascontiguousarray(in_offs, dtype=np.uint64)
+        out_offs = np.ascontiguousarray(out_offs, dtype=np.uint64)
+        sizes = np.ascontiguousarray(out_sizes, dtype=np.int64)
+        self.check(lib().lzma_dec_batch_dev_async(self.h, (ctypes.c_uint8 * 5)(*props[:5]), _dptr(d_in),
+                                                  in_offs.ctypes.data, n, sizes.ctypes.data, _dptr(d_out),
+                                                  out_offs.ctypes.data, ctypes.c_void_p(stream_ptr)))
+        self._async_n = n
+
+    def decode_batch_dev_wait(self):
+        n = getattr(self, "_async_n", 0)
+        lens = np.zeros(max(n, 1), dtype=np.uint64)
+        status = np.zeros(max(n, 1), dtype=np.int32)
+        self.check(lib().lzma_dec_batch_dev_wait(self.h, lens.ctypes.data, status.ctypes.data))
+        self._async_n = 0
+        return lens[:n], status[:n]
+
+    def set_parse_fence(self, dec_ctx: "Context | None") -> None:
+        """Encode passes on this context start their parser only after dec_ctx's
+        asynchronous decode in flight has finished (None clears it)."""
+        self.check(lib().lzma_ctx_set_parse_fence(self.h, dec_ctx.h if dec_ctx is not None else None))
 
 
 class MultiContext:
