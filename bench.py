@@ -137,7 +137,11 @@ def main():
     props = lzma_amd.write_props(p)
     ctx = lzma_amd.Context(dev.index)
     ctx.set_batch_bytes(args.batch_bytes)
-    st = torch.cuda.current_stream(dev).cuda_stream
+    # the encoder runs on a stream of its own too: work on the null stream would wait
+    # for every other stream's work (the decoder's, with --overlap)
+    torch.cuda.synchronize(dev)   # the input copy above ran on the current stream
+    enc_stream = torch.cuda.Stream(dev)
+    st = enc_stream.cuda_stream
     # the decoder gets its own context (its own device workspace) and HIP stream; with
     # --overlap a step's decode runs while the next step encodes. Every step still
     # encodes and decodes all its bytes.
@@ -455,7 +459,7 @@ def cgroup_cpus():
 def single_stream(args, full, p, dev, st, orc, op):
     """SURVEY 7.3's serial tail (config 4's regime: one stream far longer than a chunk): one
     stream of --single-stream bytes of the same data, dict as the workload, encoded and decoded
-    on the GPU (device-resident, one wave parses it: the solo kernel), beside the oracle on one
+    on the GPU (device-resident, one wave parses it), beside the oracle on one
     host thread on the same bytes; the GPU bytes must equal the oracle's."""
     n = min(args.single_stream, full.size)
     host = full[:n]

@@ -640,13 +640,18 @@ int run_match_finder(Ctx* ctx, const Derived& d, const uint8_t* in, const uint64
         if ((rc = seg_radix_sort(ctx, false, okey, w.chain_idx, okey_sorted, w.chain_order, w.son, w.son + total, w.hist, total,
                                  d_offs, nstreams, 8, st, w.seg_end, w.chain_offs))) return rc;
     }
-    uint64_t nchains = 0;   // sizes the walk grid: one host round trip per pass
-    uint32_t n_long = 0;    // the long chains (walked first)
-    if (hipMemcpyAsync(&nchains, w.chain_offs + nstreams, sizeof(nchains), hipMemcpyDeviceToHost, st) != hipSuccess ||
-        hipMemcpyAsync(&n_long, w.cls + 64, sizeof(n_long), hipMemcpyDeviceToHost, st) != hipSuccess ||
+    // sizes the walk grid: one host round trip per pass (pinned: see HostBuf)
+    if (!ctx->pin_mf.ensure(16)) return ctx->fail(LZMA_E_NOMEM, "pinned staging");
+    uint64_t* p_cnt = ctx->pin_mf.as<uint64_t>();
+    if (hipMemcpyAsync(p_cnt, w.chain_offs + nstreams, 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipMemcpyAsync(p_cnt + 1, w.cls + 64, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
         hipStreamSynchronize(st) != hipSuccess)
         return ctx->fail(LZMA_E_DEVICE, "mf: chain count: %s", hipGetErrorString(hipGetLastError()));
+    const uint64_t nchains = p_cnt[0];
+    const uint32_t n_long = (uint32_t)p_cnt[1];   // the long chains (walked first)
     LZG_TRACE(ctx, st, "mf sorts + chain lists done");
+    if (nchains > total || n_long > nchains)   // the grid below is sized from these: never launch on a bad count
+        return ctx->fail(LZMA_E_INTERNAL, "mf: chain counts %llu / %u out of range", (unsigned long long)nchains, n_long);
     if (nchains == 0) return LZMA_OK;
     if (n_long) {
         TimedLaunch tl(ctx, "mf_sort", st);
@@ -673,10 +678,10 @@ int run_match_finder(Ctx* ctx, const Derived& d, const uint8_t* in, const uint64
         }
     }
     LZG_TRACE(ctx, st, "mf_walk done (%llu chains)", (unsigned long long)nchains);
-    int herr = 0;
-    hipMemcpyAsync(&herr, w.err, sizeof(int), hipMemcpyDeviceToHost, st);
+    int32_t* p_err = (int32_t*)(p_cnt + 1);
+    hipMemcpyAsync(p_err, w.err, sizeof(int), hipMemcpyDeviceToHost, st);
     if (hipStreamSynchronize(st) != hipSuccess) return ctx->fail(LZMA_E_DEVICE, "mf_walk: %s", hipGetErrorString(hipGetLastError()));
-    if (herr) return LZMA_E_OVERFLOW;   // caller grows the overflow pool and retries
+    if (*p_err) return LZMA_E_OVERFLOW;   // caller grows the overflow pool and retries
     return LZMA_OK;
 }
 

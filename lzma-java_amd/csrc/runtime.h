@@ -90,11 +90,36 @@ struct DevBuf {
     template <typename T> T* as() const { return (T*)p; }
 };
 
+// Pinned host staging, grown on demand. Copies between the host and the device
+// go through it: a copy from pageable memory may wait for the whole device (an
+// encode on one HIP stream would then wait for a decode running on another).
+struct HostBuf {
+    void* p = nullptr;
+    size_t n = 0;
+    bool ensure(size_t want) {
+        if (want <= n) return true;
+        if (p) hipHostFree(p);
+        p = nullptr;
+        n = 0;
+        if (hipHostMalloc(&p, want, 0) != hipSuccess) return false;
+        n = want;
+        return true;
+    }
+    void release() {
+        if (p) hipHostFree(p);
+        p = nullptr;
+        n = 0;
+    }
+    template <typename T> T* as(size_t byte_off = 0) const { return (T*)((uint8_t*)p + byte_off); }
+};
+
 struct Ctx {
     uint32_t magic = kCtxMagic;   // first member: see kCtxMagic
     int device = 0;
     // host-buffer entry points (lzma_enc_batch, lzma_dec_batch, lzma_match_lists): staging in HBM
     DevBuf io_in, io_out, io_pack, io_offs;
+    HostBuf pin;        // encode-pass and pack staging (offsets, order, lengths, status)
+    HostBuf pin_mf;     // the match finder's chain-count readback
     std::string err;
     bool debug = getenv("LZMA_MI355X_DEBUG") != nullptr;   // phase trace on stderr (synchronises)
     uint64_t batch_bytes = 512ull << 20;
@@ -110,6 +135,7 @@ struct Ctx {
     size_t dec_host_words = 0;
     int dec_pending = 0;             // streams of the decode in flight (0 = none)
     hipEvent_t dec_done = nullptr;
+    hipStream_t dec_stream = nullptr;
     // parse fence (lzma_ctx_set_parse_fence): an encode pass waits for this
     // context's decode in flight before it launches its parser
     const Ctx* fence = nullptr;

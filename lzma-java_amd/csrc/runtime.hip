@@ -198,14 +198,28 @@ static int encode_pass(Ctx* ctx, const Derived& d, const uint8_t* d_in, const ui
         }
         Carver c(ctx->arena);
         need(c, w, &inpad, &d_offs, &d_oofs, &d_order, &d_lens, &d_status, &d_next, &d_scr);
+        // host arrays go through pinned staging (see HostBuf): the pass syncs on its
+        // lengths at the end, so the staging is free again when the next pass starts
+        const size_t pn = (size_t)ns + 1;
+        if (!ctx->pin.ensure(pn * 8 * 5 + pn * 4 * 2)) return ctx->fail(LZMA_E_NOMEM, "pinned staging");
+        uint64_t* p_offs = ctx->pin.as<uint64_t>();
+        uint64_t* p_oofs = p_offs + pn;
+        uint64_t* p_rofs = p_oofs + pn;
+        uint64_t* p_lens = p_rofs + pn;
+        uint32_t* p_order = (uint32_t*)(p_lens + pn);
+        int32_t* p_status = (int32_t*)(p_order + pn);
+        memcpy(p_offs, offs.data(), pn * 8);
+        memcpy(p_oofs, oofs.data(), pn * 8);
+        memcpy(p_rofs, rofs.data(), pn * 8);
+        memcpy(p_order, order.data(), (size_t)ns * 4);
         {
             TimedLaunch tl(ctx, "enc_stage", st);
             HIPCHK(hipMemcpyAsync(inpad, d_in + in0, total, hipMemcpyDeviceToDevice, st));
             HIPCHK(hipMemsetAsync(inpad + total, 0, 512, st));
-            HIPCHK(hipMemcpyAsync(d_offs, offs.data(), (ns + 1) * 8, hipMemcpyHostToDevice, st));
-            HIPCHK(hipMemcpyAsync(d_oofs, oofs.data(), (ns + 1) * 8, hipMemcpyHostToDevice, st));
-            HIPCHK(hipMemcpyAsync(d_order, order.data(), ns * 4, hipMemcpyHostToDevice, st));
-            HIPCHK(hipMemcpyAsync(d_rofs, rofs.data(), (ns + 1) * 8, hipMemcpyHostToDevice, st));
+            HIPCHK(hipMemcpyAsync(d_offs, p_offs, pn * 8, hipMemcpyHostToDevice, st));
+            HIPCHK(hipMemcpyAsync(d_oofs, p_oofs, pn * 8, hipMemcpyHostToDevice, st));
+            HIPCHK(hipMemcpyAsync(d_order, p_order, ns * 4, hipMemcpyHostToDevice, st));
+            HIPCHK(hipMemcpyAsync(d_rofs, p_rofs, pn * 8, hipMemcpyHostToDevice, st));
             HIPCHK(hipMemsetAsync(d_next, 0, 16, st));
         }
         int rc = run_match_finder(ctx, d, inpad, d_offs, ns, total, wide, w, st);
@@ -222,9 +236,9 @@ static int encode_pass(Ctx* ctx, const Derived& d, const uint8_t* d_in, const ui
             dump->stride = (uint32_t)stride;
             dump->ovf_off.resize(total);
             dump->recs.resize(total * rec_bytes(wide));
-            unsigned long long used = 0;
-            HIPCHK(hipMemcpyAsync(&used, w.ovf_used, sizeof used, hipMemcpyDeviceToHost, st));
+            HIPCHK(hipMemcpyAsync(p_lens, w.ovf_used, 8, hipMemcpyDeviceToHost, st));
             HIPCHK(hipStreamSynchronize(st));
+            const unsigned long long used = p_lens[0];
             dump->ovf.resize(std::min<uint64_t>(used * stride, ovf_cap) * psz);
             if (total) {
                 HIPCHK(hipMemcpyAsync(dump->ovf_off.data(), w.ovf_off, total * 4, hipMemcpyDeviceToHost, st));
@@ -270,9 +284,11 @@ static int encode_pass(Ctx* ctx, const Derived& d, const uint8_t* d_in, const ui
         report_profile(d_prof, ns, total, st);
         hipFree(d_prof);
 #endif
-        HIPCHK(hipMemcpyAsync(h_out_lens + s0, d_lens, ns * 8, hipMemcpyDeviceToHost, st));
-        HIPCHK(hipMemcpyAsync(h_status + s0, d_status, ns * 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipMemcpyAsync(p_lens, d_lens, ns * 8, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipMemcpyAsync(p_status, d_status, ns * 4, hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
+        memcpy(h_out_lens + s0, p_lens, (size_t)ns * 8);
+        memcpy(h_status + s0, p_status, (size_t)ns * 4);
         return LZMA_OK;
     }
     return ctx->fail(LZMA_E_NOMEM, "match-pair overflow pool kept overflowing");
@@ -361,22 +377,23 @@ static int decode_enqueue(Ctx* ctx, const uint8_t props[5], const uint8_t* d_in,
     a.lit_in_lds = lit_lds;
     int rc = launch_decoder(ctx, a, grid, st);
     if (rc) return rc;
-    HIPCHK(hipMemcpyAsync(h_out_lens, d_lens, nstreams * 8, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(h_status, d_status, nstreams * 4, hipMemcpyDeviceToHost, st));
+    if (h_out_lens) HIPCHK(hipMemcpyAsync(h_out_lens, d_lens, nstreams * 8, hipMemcpyDeviceToHost, st));
+    if (h_status) HIPCHK(hipMemcpyAsync(h_status, d_status, nstreams * 4, hipMemcpyDeviceToHost, st));
     return LZMA_OK;
 }
+
+static int decode_batch_dev_async(Ctx* ctx, const uint8_t props[5], const uint8_t* d_in, const uint64_t* h_in_offs,
+                                  int nstreams, const int64_t* h_out_sizes, uint8_t* d_out, const uint64_t* h_out_offs,
+                                  hipStream_t st);
+static int decode_batch_dev_wait(Ctx* ctx, uint64_t* h_out_lens, int32_t* h_status);
 
 static int decode_batch_dev(Ctx* ctx, const uint8_t props[5], const uint8_t* d_in, const uint64_t* h_in_offs, int nstreams,
                             const int64_t* h_out_sizes, uint8_t* d_out, const uint64_t* h_out_offs, uint64_t* h_out_lens,
                             int32_t* h_status, hipStream_t st) {
     if (ctx->dec_pending) return ctx->fail(LZMA_E_PARAM, "an asynchronous decode is in flight: lzma_dec_batch_dev_wait first");
-    if (nstreams <= 0) return nstreams == 0 ? LZMA_OK : ctx->fail(LZMA_E_PARAM, "nstreams < 0");
-    std::vector<uint32_t> order(nstreams);
-    int rc = decode_enqueue(ctx, props, d_in, h_in_offs, nstreams, h_out_sizes, d_out, h_out_offs, h_out_lens, h_status,
-                            order.data(), st);
+    int rc = decode_batch_dev_async(ctx, props, d_in, h_in_offs, nstreams, h_out_sizes, d_out, h_out_offs, st);
     if (rc) return rc;
-    HIPCHK(hipStreamSynchronize(st));
-    return LZMA_OK;
+    return decode_batch_dev_wait(ctx, h_out_lens, h_status);
 }
 
 // The asynchronous form: every host array is staged in the context's pinned
@@ -407,10 +424,14 @@ static int decode_batch_dev_async(Ctx* ctx, const uint8_t props[5], const uint8_
     memcpy(in_offs, h_in_offs, (n + 1) * 8);
     memcpy(sizes, h_out_sizes, n * 8);
     memcpy(out_offs, h_out_offs, (n + 1) * 8);
-    int rc = decode_enqueue(ctx, props, d_in, in_offs, nstreams, sizes, d_out, out_offs, lens, status, order, st);
+    // no device-to-host copy is queued behind the kernel: a copy waiting on the decode
+    // would hold the copy engine, and other streams' copies would queue behind it
+    // until the decode ends (_wait copies the results once the kernel is done)
+    int rc = decode_enqueue(ctx, props, d_in, in_offs, nstreams, sizes, d_out, out_offs, nullptr, nullptr, order, st);
     if (rc) return rc;
     HIPCHK(hipEventRecord(ctx->dec_done, st));
     ctx->dec_pending = nstreams;
+    ctx->dec_stream = st;
     return LZMA_OK;
 }
 
@@ -419,8 +440,17 @@ static int decode_batch_dev_wait(Ctx* ctx, uint64_t* h_out_lens, int32_t* h_stat
     const size_t n = (size_t)ctx->dec_pending;
     ctx->dec_pending = 0;
     HIPCHK(hipEventSynchronize(ctx->dec_done));
-    const uint64_t* lens = ctx->dec_host + (n + 1) * 3;
-    const int32_t* status = (const int32_t*)((const uint32_t*)(lens + n) + (n + 1) / 2 * 2);
+    uint64_t* lens = ctx->dec_host + (n + 1) * 3;
+    int32_t* status = (int32_t*)((uint32_t*)(lens + n) + (n + 1) / 2 * 2);
+    {   // the decoder's outputs sit at the front of the arena (decode_enqueue's carving)
+        Carver c(ctx->arena);
+        c.take<uint64_t>(n + 1); c.take<int64_t>(n); c.take<uint64_t>(n + 1);
+        const uint64_t* d_lens = c.take<uint64_t>(n);
+        const int32_t* d_status = c.take<int32_t>(n);
+        HIPCHK(hipMemcpyAsync(lens, d_lens, n * 8, hipMemcpyDeviceToHost, ctx->dec_stream));
+        HIPCHK(hipMemcpyAsync(status, d_status, n * 4, hipMemcpyDeviceToHost, ctx->dec_stream));
+        HIPCHK(hipStreamSynchronize(ctx->dec_stream));
+    }
     if (h_out_lens) memcpy(h_out_lens, lens, n * 8);
     if (h_status) memcpy(h_status, status, n * 4);
     return LZMA_OK;
@@ -504,6 +534,7 @@ void lzma_ctx_destroy(lzma_ctx* ctx) {
     if (ctx->litbuf) hipFree(ctx->litbuf);
     if (ctx->tmp) hipFree(ctx->tmp);
     ctx->io_in.release(); ctx->io_out.release(); ctx->io_pack.release(); ctx->io_offs.release();
+    ctx->pin.release(); ctx->pin_mf.release();
     ctx->magic = 0;
     delete ctx;
 }
@@ -567,8 +598,13 @@ int lzma_pack_dev(lzma_ctx* ctx, const uint8_t* d_src, const uint64_t* h_src_off
     Carver c(ctx->arena);
     uint64_t* d_so = c.take<uint64_t>(nstreams + 1);
     uint64_t* d_do = c.take<uint64_t>(nstreams + 1);
-    HIPCHK(hipMemcpyAsync(d_so, h_src_offs, (nstreams + 1) * 8, hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(d_do, h_dst_offs, (nstreams + 1) * 8, hipMemcpyHostToDevice, st));
+    if (!ctx->pin.ensure((size_t)(nstreams + 1) * 16)) return ctx->fail(LZMA_E_NOMEM, "pinned staging");
+    uint64_t* p_so = ctx->pin.as<uint64_t>();
+    uint64_t* p_do = p_so + nstreams + 1;
+    memcpy(p_so, h_src_offs, (size_t)(nstreams + 1) * 8);
+    memcpy(p_do, h_dst_offs, (size_t)(nstreams + 1) * 8);
+    HIPCHK(hipMemcpyAsync(d_so, p_so, (nstreams + 1) * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(d_do, p_do, (nstreams + 1) * 8, hipMemcpyHostToDevice, st));
     {
         TimedLaunch tl(ctx, "pack", st);
         hipLaunchKernelGGL(pack_kernel, dim3(std::min(nstreams, 65535)), dim3(256), 0, st, d_src, d_so, d_do, d_dst, nstreams);
