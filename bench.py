@@ -68,10 +68,6 @@ def parse():
                     help="streams each rank checks against the oracle (-1 = every stream; at N=1 the "
                          "cpu_baseline sample's oracle bytes are reused and the rest encoded beside them)")
     ap.add_argument("--no-verify", action="store_true")
-    ap.add_argument("--overlap", action="store_true",
-                    help="pipeline the steps: the decode of step k runs on its own HIP stream and context beside "
-                         "step k+1's match finder; step k+1's parser starts when that decode is done "
-                         "(default: each step's encode and decode run back to back)")
     return ap.parse_args()
 
 
@@ -138,37 +134,23 @@ def main():
     ctx = lzma_amd.Context(dev.index)
     ctx.set_batch_bytes(args.batch_bytes)
     # the encoder runs on a stream of its own too: work on the null stream would wait
-    # for every other stream's work (the decoder's, with --overlap)
+    # for every other stream's work
     torch.cuda.synchronize(dev)   # the input copy above ran on the current stream
     enc_stream = torch.cuda.Stream(dev)
     st = enc_stream.cuda_stream
-    # the decoder gets its own context (its own device workspace) and HIP stream; with
-    # --overlap a step's decode runs while the next step encodes. Every step still
-    # encodes and decodes all its bytes.
+    # the decoder gets its own context (its own device workspace) and HIP stream
     ctx_dec = lzma_amd.Context(dev.index)
     dec_stream = torch.cuda.Stream(dev)
     st_dec = dec_stream.cuda_stream
 
     state = {"dec_ok": True}
-    if args.overlap:   # the parse of step k+1 waits for step k's decode (lzma_ctx_set_parse_fence)
-        ctx.set_parse_fence(ctx_dec)
 
     def decode(buf, pk):
         t1 = time.perf_counter()
-        if args.overlap:
-            ctx_dec.decode_batch_dev_async(props, buf, pk, out_sizes, d_dec, offs, st_dec)
-            state["dec_inflight"] = True
-        else:
-            dlens, dstat = ctx_dec.decode_batch_dev(props, buf, pk, out_sizes, d_dec, offs, st_dec)
-            state["dstat"], state["dlens"] = dstat, dlens
-            state["dec_ok"] &= bool((dstat == 0).all()) and bool((dlens == out_sizes).all())
+        dlens, dstat = ctx_dec.decode_batch_dev(props, buf, pk, out_sizes, d_dec, offs, st_dec)
+        state["dstat"], state["dlens"] = dstat, dlens
+        state["dec_ok"] &= bool((dstat == 0).all()) and bool((dlens == out_sizes).all())
         state["t_dec"] = state.get("t_dec", 0.0) + (time.perf_counter() - t1)
-
-    def join():
-        if state.pop("dec_inflight", False):
-            dlens, dstat = ctx_dec.decode_batch_dev_wait()
-            state["dstat"], state["dlens"] = dstat, dlens
-            state["dec_ok"] &= bool((dstat == 0).all()) and bool((dlens == out_sizes).all())
 
     def step(k):
         t0 = time.perf_counter()
@@ -180,12 +162,10 @@ def main():
             state["gathered"] = 0 if g is None else int(g.numel())
         state["lens"], state["pk"], state["buf"] = lens, pk, buf
         state["t_enc"] = state.get("t_enc", 0.0) + (time.perf_counter() - t0)
-        join()   # the previous step's decode (done: this step's parse waited for it)
         decode(buf, pk)
 
     for k in range(args.warmup):
         step(k)
-    join()
 
     def barrier():
         if dist:
@@ -200,7 +180,6 @@ def main():
     t0 = time.perf_counter()
     for k in range(args.steps):
         step(k)
-    join()
     barrier()
     elapsed = time.perf_counter() - t0
     timings = ctx.timings()
@@ -272,9 +251,6 @@ def main():
                 "alg_bytes_per_launch": alg, "issue": issue_bound(dname, wl, avg_s, my_size)}
 
     t_enc, t_dec = state["t_enc"], state["t_dec"]
-    if args.overlap:
-        t_dec = sum(v[0] for k_, v in timings.items() if k_ == "dec_stream") / 1e3
-        t_enc = sum(v[0] for k_, v in timings.items() if k_ != "dec_stream") / 1e3
     if rank == 0:
         desc = "LzmaBench generator" if args.data == "bench" else "TEXT (enwik9-shaped) generator"
         res = {
@@ -292,10 +268,7 @@ def main():
             "compress_MBps": my_size * world * args.steps / max(t_enc, 1e-9) / 1e6,
             "decompress_MBps": my_size * world * args.steps / max(t_dec, 1e-9) / 1e6,
             "schedule": "sequential: each step's encode and decode back to back; compress/decompress MB/s are "
-                        "each phase's wall time" if not args.overlap else
-                        "pipelined: step k's decode (own context + HIP stream) runs beside step k+1's match finder, "
-                        "step k+1's parser waits for it; compress/decompress MB/s are each phase's summed kernel "
-                        "times (HIP events), which overlap",
+                        "each phase's wall time",
             "ratio": comp_bytes / max(my_size, 1), "verified": ok,
             "verified_means": "every stream decodes to its input and every sampled stream's bytes equal the "
                               "oracle's Encoder.Code restatement",

@@ -538,8 +538,11 @@ __global__ void __launch_bounds__(64) LZG_WALK_ATTR mf_walk_kernel(const uint8_t
                 }
             }
             const uint64_t node = ((uint64_t)cur_match << 32) | (uint32_t)(cur_idx + 1);
-            const uint64_t nxt = pby_less ? nd.s1 : nd.s0;
+            uint64_t nxt = pby_less ? nd.s1 : nd.s0;
             uint64_t* const here = pby_less ? &nodes[cur_idx].s1 : &nodes[cur_idx].s0;
+            // a link always names an earlier member of this bucket: anything else is a
+            // consistency failure, reported instead of followed
+            if (nxt != 0 && ((uint64_t)(uint32_t)nxt - 1 < start || (uint64_t)(uint32_t)nxt - 1 >= i)) { *err = 3; nxt = 0; }
             if (nxt != 0) nd = nodes[(uint32_t)nxt - 1];   // issued before this step's stores
             if (pby_less) { if (prev_dir != 2) put1(node); ptr1 = here; p1_self = false; len1 = len; prev_dir = 2; }
             else { if (prev_dir != 1) put0(node); ptr0 = here; p0_self = false; len0 = len; prev_dir = 1; }
@@ -681,6 +684,7 @@ int run_match_finder(Ctx* ctx, const Derived& d, const uint8_t* in, const uint64
     int32_t* p_err = (int32_t*)(p_cnt + 1);
     hipMemcpyAsync(p_err, w.err, sizeof(int), hipMemcpyDeviceToHost, st);
     if (hipStreamSynchronize(st) != hipSuccess) return ctx->fail(LZMA_E_DEVICE, "mf_walk: %s", hipGetErrorString(hipGetLastError()));
+    if (*p_err == 3) return ctx->fail(LZMA_E_INTERNAL, "mf_walk: a tree link outside its bucket");
     if (*p_err) return LZMA_E_OVERFLOW;   // caller grows the overflow pool and retries
     return LZMA_OK;
 }
