@@ -125,12 +125,17 @@ constexpr Tables make_tables() {
 // quarter gets priority 3, the fastest 0. Slots hold progress + 1, 0 = empty.
 // Table rows: 2048 CUs (xcc, se, sh, cu of HW_ID / XCC_ID) x 64 waves (simd, wave).
 constexpr uint32_t kSchedRows = 2048, kSchedCols = 64;
+#if LZG_WAVE == 64 && !defined(LZG_NO_FAIRPRIO)
+#define LZG_FAIRPRIO 1   // -DLZG_NO_FAIRPRIO: an experiment build without it
+#else
+#define LZG_FAIRPRIO 0
+#endif
 struct FairPrio {
     uint32_t* row;
     uint32_t slot, next, step;
     float scale;
     __device__ inline void start(uint32_t* table, uint32_t len, uint32_t lane) {
-#if LZG_WAVE == 64
+#if LZG_FAIRPRIO
         const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);           // HW_REG_HW_ID
         const uint32_t xcc = __builtin_amdgcn_s_getreg((15 << 11) | 20) & 7u;   // HW_REG_XCC_ID
         const uint32_t cu = (((xcc * 8u + ((hw >> 13) & 7u)) * 2u + ((hw >> 12) & 1u)) * 16u) + ((hw >> 8) & 15u);
@@ -146,7 +151,7 @@ struct FairPrio {
 #endif
     }
     __device__ inline void update(uint32_t pos, uint32_t lane) {
-#if LZG_WAVE == 64
+#if LZG_FAIRPRIO
         if (pos < next) return;
         next = pos + step;
         const uint32_t prog = (uint32_t)((float)pos * scale) + 1u;
@@ -166,7 +171,7 @@ struct FairPrio {
 #endif
     }
     __device__ inline void finish(uint32_t lane) {
-#if LZG_WAVE == 64
+#if LZG_FAIRPRIO
         if (lane == 0) __hip_atomic_store(row + slot, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #else
         (void)lane;
