@@ -293,6 +293,8 @@ _KERNEL_OF = {"enc_parse": "enc_kernel", "dec_stream": "dec_kernel", "mf_walk": 
 def _profile(name, wl):
     """A committed per-kernel summary from profiles/ (written by tools/profile_round.sh
     over this same workload), or None when absent or taken on another workload."""
+    if wl.get("data") == "text":   # config 3's own summaries (tools/profile_r03.sh text)
+        name = "r03/text_" + name
     path = os.path.join(REPO, "profiles", name)
     if not os.path.exists(path):
         return None
@@ -315,7 +317,8 @@ def pmc_traffic(label, wl):
     prefix = _KERNEL_OF.get(label, label)
     for k, v in t.items():
         if k.startswith(prefix) and isinstance(v, dict) and "traffic_bytes_per_launch" in v:
-            return v["traffic_bytes_per_launch"], "profiles/traffic.json (%s, rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)" % k
+            return v["traffic_bytes_per_launch"], "profiles/%straffic.json (%s, rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)" % (
+                "r03/text_" if wl.get("data") == "text" else "", k)
     return None, None
 
 

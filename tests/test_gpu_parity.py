@@ -215,6 +215,21 @@ def test_gpu_device_resident_api(ctx):
                                       (offs[1:] - offs[:-1]).astype(np.int64), d_dec, offs, st)
     assert (dst == 0).all()
     assert torch.equal(d_dec.cpu(), torch.from_numpy(data))
+    # the asynchronous form on a context of its own and a HIP stream of its own: the
+    # call returns once enqueued, _wait gives the same lengths and verdicts
+    dctx = lzma_amd.Context(0)
+    try:
+        s2 = torch.cuda.Stream()
+        d_dec.zero_()
+        torch.cuda.synchronize()
+        dctx.decode_batch_dev_async(lzma_amd.write_props(p), packed, in_offs,
+                                    (offs[1:] - offs[:-1]).astype(np.int64), d_dec, offs, s2.cuda_stream)
+        alens, ast = dctx.decode_batch_dev_wait()
+        assert (ast == 0).all() and np.array_equal(alens, dlens)
+        torch.cuda.synchronize()
+        assert torch.equal(d_dec.cpu(), torch.from_numpy(data))
+    finally:
+        dctx.close()
 
 
 # ---------------------------------------------------------------- match lists (SURVEY 7.1 instrumented mode)
