@@ -320,6 +320,15 @@ struct Dec {
                 bool same = matched;
                 // unrolled: level i's nodes are [2^i, 2^(i+1)), so levels 0-6 read the
                 // low lane vector only (a static choice)
+                if (!matched) {   // DecodeNormal: no match-byte bookkeeping per bit
+#pragma unroll
+                    for (uint32_t i = 0; i < 8; i++) {
+                        uint32_t np;
+                        const uint32_t x = dbit(node256(tt, sym, (int)i), &np);
+                        sub[sym] = (uint16_t)np;
+                        sym = (sym << 1) | x;
+                    }
+                } else
 #pragma unroll
                 for (uint32_t i = 0; i < 8; i++) {
                     uint32_t np, idx, prob;
