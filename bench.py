@@ -9,23 +9,36 @@ generator at dict 2^28 (config 3). A step = encode every stream (GPU), pack
 the outputs into one contiguous buffer (GPU), decode every stream (GPU).
 Inputs are resident in HBM before the timed region.
 
-Multi-GPU: one process per GPU. Weak scaling (default):
-every rank encodes its own 1 GiB. Strong scaling (--strong, north_star's
-"one 1 GB buffer at 1, 2, 4 and 8 GPUs"): the 1 GiB buffer's streams are
-dealt round-robin, rank r taking {i : i mod G = r}. Either way there is no
-data-path collective; the step ends with the one exchange 8(e) prescribes:
-rank 0 gathers every rank's packed streams over RCCL.
+Multi-GPU (north_star's "one 1 GB buffer at 1, 2, 4 and 8
+GPUs"): one process per GPU. `--gpus N` without WORLD_SIZE in the environment
+starts the N rank processes itself (before any GPU call); under
+torch.distributed.run the ranks come from the environment. `value` is STRONG
+scaling: one --size buffer whose streams are dealt round-robin, rank r taking
+{i : i mod G = r}, value = the buffer's bytes / the max-over-ranks step time.
+At N > 1 a second timed pass gives the weak-scaling figure (every rank its own
+--size buffer) as the extra key `weak_scaling`. Neither has a data-path
+collective; each step ends with the one exchange 8(e) prescribes: rank 0
+gathers every rank's packed streams over RCCL, and after the timed loop checks
+that the multi-member container holds every stream of the buffer.
 
 Parity: `verified` is true only if every stream decodes back to its input
 AND every sampled stream's GPU bytes equal the oracle's (the bit-exact C
 restatement of Encoder.Code) -- at N=1 the sample is the cpu_baseline's
-(spread over the whole buffer), at N>1 each rank checks its own sample.
+(spread over the whole buffer) plus the rest of the buffer, at N>1 each rank
+checks its own streams.
+
+`--emulate` (CPU tests only): the same code path with CPU tensors, the gloo
+backend and the product kernels compiled for the CPU SIMT emulation
+(tests/simt, LZMA_AMD_LIB); it measures nothing and exists so that the
+launcher, the round-robin deal and the gather run in the CPU test suite.
 
 Prints ONE JSON line (rank 0).
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -38,6 +51,7 @@ import lzma_amd  # noqa: E402
 from lzma_amd import dist as lzdist  # noqa: E402
 
 HBM_PEAK = 8.0e12   # MI355X HBM3E, MI355X_MICROARCH.md chip-level parameters
+SIMT_LIB = os.path.join(REPO, "tests", "simt", "build", "so", "libsimt_lzma.so")
 
 
 def parse():
@@ -45,13 +59,14 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--size", type=int, default=1 << 30, help="uncompressed bytes (per GPU; per job with --strong)")
+    ap.add_argument("--size", type=int, default=1 << 30,
+                    help="uncompressed bytes of the job's buffer (strong scaling; per GPU in the weak pass)")
     ap.add_argument("--chunk", type=int, default=256 << 10, help="bytes per independent stream")
     ap.add_argument("--data", choices=["bench", "text"], default="bench",
                     help="bench: LzmaBench generator (configs 2/4); text: enwik9-shaped TEXT (config 3)")
     ap.add_argument("--dict-log", type=int, default=None, help="log2 dictionary size (default 26; 28 with --data text)")
-    ap.add_argument("--strong", action="store_true",
-                    help="strong scaling: one --size buffer, streams dealt round-robin over the ranks")
+    ap.add_argument("--strong", action="store_true", help="(kept for old command lines: strong scaling is the default)")
+    ap.add_argument("--no-weak", action="store_true", help="N > 1: skip the weak-scaling pass")
     ap.add_argument("--batch-bytes", type=int, default=1 << 30,
                     help="input bytes per device pass (1 GiB: all streams of a GPU in one encoder launch)")
     ap.add_argument("--cpu-sample", type=int, default=128 << 20,
@@ -68,6 +83,10 @@ def parse():
                     help="streams each rank checks against the oracle (-1 = every stream; at N=1 the "
                          "cpu_baseline sample's oracle bytes are reused and the rest encoded beside them)")
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--emulate", action="store_true",
+                    help="CPU tests only: CPU tensors, gloo and the SIMT-emulated product kernels (measures nothing)")
+    ap.add_argument("--dump-container", default=None,
+                    help="rank 0 writes the gathered multi-member container of the strong pass to this path")
     return ap.parse_args()
 
 
@@ -78,39 +97,86 @@ def spread(n, k):
     return sorted(set(int(i) for i in np.linspace(0, n - 1, k).round()))
 
 
-def make_input(args, rank, world):
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(args):
+    """`--gpus N` outside torch.distributed.run: start one rank process per GPU with
+    RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set (rendezvous on 127.0.0.1), before
+    this process makes any GPU call, and exit with the first failing rank's code.
+    If a rank fails, the others (which would wait in a collective) are stopped."""
+    n = args.gpus
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code and not rc:
+                rc = code
+                for q in live:   # the ranks this launcher started, by their own handles
+                    q.terminate()
+        time.sleep(0.2)
+    return rc
+
+
+class Device:
+    """The rank's device: one MI355X (HIP streams from torch), or the CPU under --emulate."""
+
+    def __init__(self, emulate, local):
+        self.emulate = emulate
+        if emulate:
+            self.dev = torch.device("cpu")
+            self.index = 0
+        else:
+            torch.cuda.set_device(local)
+            self.dev = torch.device("cuda", local)
+            self.index = local
+
+    def sync(self):
+        if not self.emulate:
+            torch.cuda.synchronize(self.dev)
+
+    def new_stream(self):
+        # the encoder and decoder run on HIP streams of their own: work on the null stream
+        # would wait for every other stream's work
+        return 0 if self.emulate else torch.cuda.Stream(self.dev).cuda_stream
+
+
+def make_input(args, rank, world, strong):
+    """The rank's whole buffer: one shared buffer (strong), or its own (weak; rank 0's
+    equals the shared one, so at N = 1 both passes are the same workload)."""
     size = args.size
     if args.data == "text":
-        seed = 1 if args.strong else 1 + rank
-        return lzma_amd.text_generate(size, seed)
+        return lzma_amd.text_generate(size, 1 if strong else 1 + rank)
     host = lzma_amd.bench_generate(size)
-    if rank and not args.strong:   # distinct streams per rank: the generator output rotated by an odd offset
+    if rank and not strong:   # distinct streams per rank: the generator output rotated by an odd offset
         host = np.roll(host, -(rank * 262147) % size)
     return host
 
 
-def main():
-    args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = world > 1
-    if dist:
-        import torch.distributed as td
-        torch.cuda.set_device(local)
-        td.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(0)
-    dev = torch.device("cuda", torch.cuda.current_device())
-    dict_log = args.dict_log if args.dict_log is not None else (28 if args.data == "text" else 26)
-
-    # ---- synthetic data (host gen, then H2D; outside the timed region)
-    full = make_input(args, rank, world)
+def run_pass(args, D, p, ctxs, strong, rank, world, dist):
+    """Warm-up + timed steps of one scaling mode; returns its measurements."""
+    ctx, ctx_dec, st, st_dec = ctxs
+    full = make_input(args, rank, world, strong)
     size = full.size
     n_all = (size + args.chunk - 1) // args.chunk
     all_offs = np.minimum(np.arange(n_all + 1, dtype=np.uint64) * np.uint64(args.chunk), np.uint64(size))
-    mine = lzdist.rank_streams(n_all, rank, world) if args.strong else np.arange(n_all)
-    if args.strong:
+    mine = lzdist.rank_streams(n_all, rank, world) if strong else np.arange(n_all)
+    if strong and world > 1:
         host = np.concatenate([full[int(all_offs[i]):int(all_offs[i + 1])] for i in mine]) if mine.size else full[:0]
     else:
         host = full
@@ -119,36 +185,21 @@ def main():
     n = int(mine.size)
     offs = np.zeros(n + 1, dtype=np.uint64)
     offs[1:] = np.cumsum(lens_in)
-    d_in = torch.from_numpy(host).to(dev)
+    d_in = torch.from_numpy(np.ascontiguousarray(host)).to(D.dev)
     caps = np.array([lzma_amd.enc_bound(int(x)) for x in lens_in], dtype=np.uint64)
     cap_offs = np.zeros(n + 1, dtype=np.uint64)
     cap_offs[1:] = np.cumsum(caps)
-    d_comp = torch.empty(int(cap_offs[-1]) + 1, dtype=torch.uint8, device=dev)
-    # two packed buffers: step k's decode reads one while step k+1 packs into the other
-    d_packs = [torch.empty(int(cap_offs[-1]) + 1, dtype=torch.uint8, device=dev) for _ in range(2)]
-    d_dec = torch.empty(my_size + 1, dtype=torch.uint8, device=dev)
+    d_comp = torch.empty(int(cap_offs[-1]) + 1, dtype=torch.uint8, device=D.dev)
+    d_packs = [torch.empty(int(cap_offs[-1]) + 1, dtype=torch.uint8, device=D.dev) for _ in range(2)]
+    d_dec = torch.empty(my_size + 1, dtype=torch.uint8, device=D.dev)
     out_sizes = lens_in.astype(np.int64)
-
-    p = lzma_amd.make_params(dict_size=1 << dict_log, fb=32, mf=1, lc=3, lp=0, pb=2)
     props = lzma_amd.write_props(p)
-    ctx = lzma_amd.Context(dev.index)
-    ctx.set_batch_bytes(args.batch_bytes)
-    # the encoder runs on a stream of its own too: work on the null stream would wait
-    # for every other stream's work
-    torch.cuda.synchronize(dev)   # the input copy above ran on the current stream
-    enc_stream = torch.cuda.Stream(dev)
-    st = enc_stream.cuda_stream
-    # the decoder gets its own context (its own device workspace) and HIP stream
-    ctx_dec = lzma_amd.Context(dev.index)
-    dec_stream = torch.cuda.Stream(dev)
-    st_dec = dec_stream.cuda_stream
-
+    D.sync()   # the input copy above ran on the current stream
     state = {"dec_ok": True}
 
     def decode(buf, pk):
         t1 = time.perf_counter()
         dlens, dstat = ctx_dec.decode_batch_dev(props, buf, pk, out_sizes, d_dec, offs, st_dec)
-        state["dstat"], state["dlens"] = dstat, dlens
         state["dec_ok"] &= bool((dstat == 0).all()) and bool((dlens == out_sizes).all())
         state["t_dec"] = state.get("t_dec", 0.0) + (time.perf_counter() - t1)
 
@@ -158,20 +209,19 @@ def main():
         buf = d_packs[k % 2]
         pk = ctx.pack_dev(d_comp, cap_offs, lens, buf, st)   # synchronous: buf is complete
         if dist:   # the single data exchange: rank 0 collects every rank's packed streams
-            g, _, _ = lzdist.gather_streams(buf, lens, dst=0)
-            state["gathered"] = 0 if g is None else int(g.numel())
+            g, all_lens, counts = lzdist.gather_streams(buf, lens, dst=0)
+            state["gathered"] = None if g is None else (g, all_lens, counts)
         state["lens"], state["pk"], state["buf"] = lens, pk, buf
         state["t_enc"] = state.get("t_enc", 0.0) + (time.perf_counter() - t0)
         decode(buf, pk)
 
-    for k in range(args.warmup):
-        step(k)
-
     def barrier():
         if dist:
             torch.distributed.barrier()
-        torch.cuda.synchronize(dev)
+        D.sync()
 
+    for k in range(args.warmup):
+        step(k)
     for c in (ctx, ctx_dec):
         c.set_timing(True)
         c.reset_timings()
@@ -186,54 +236,138 @@ def main():
     timings.update(ctx_dec.timings())
     for c in (ctx, ctx_dec):
         c.set_timing(False)
-
     if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=D.dev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t.item())
-
     comp_bytes = int(np.sum(state["lens"]))
     roundtrip = state["dec_ok"]
     if not args.no_verify:
         roundtrip = roundtrip and bool(torch.equal(d_dec[:my_size], d_in))
-
-    # ---- CPU baseline (rank 0, N = 1) and the oracle parity sample
-    cpu, ref = None, {}
-    op = None
-    if not args.no_verify or (rank == 0 and world == 1 and args.cpu_sample > 0):
-        sys.path.insert(0, os.path.join(REPO, "tests"))
-        import oracle_ffi as orc
-        op = orc.params(p.dict_size, p.fb, p.mf, p.lc, p.lp, p.pb, p.eos)
-        chunks = [host[int(offs[i]):int(offs[i + 1])] for i in range(n)]
-        if rank == 0 and world == 1 and args.cpu_sample > 0:
-            cpu, ref = cpu_baseline(orc, op, chunks, args)
-        if not args.no_verify:
-            want = range(n) if args.parity_streams < 0 else spread(n, args.parity_streams)
-            idx = [i for i in want if i not in ref]
-            if idx:   # not timed: the parity check of the streams the baseline sample did not cover
-                outs = orc.encode_many([chunks[i].tobytes() for i in idx], op, threads=orc.cpu_threads())
-                ref.update(zip(idx, outs))
-    parity_ok, checked = True, 0
-    if ref:
+    gathered = None
+    if dist:
+        # the gather's check (after the timed loop): every rank's per-stream CRC-32 of what it
+        # packed, against the streams rank 0 received; then the multi-member container
+        import zlib
         host_pack = state["buf"][:comp_bytes].cpu().numpy()
         pk = state["pk"]
-        for i, r in ref.items():
+        mine_crc = [zlib.crc32(host_pack[int(pk[i]):int(pk[i + 1])]) for i in range(n)]
+        every = [None] * world
+        torch.distributed.all_gather_object(every, mine_crc)
+        if rank == 0:
+            g, all_lens, counts = state["gathered"]
+            gb = g.cpu().numpy()
+            goffs = np.concatenate([[0], np.cumsum(all_lens)]).astype(np.int64)
+            got_crc = [zlib.crc32(gb[int(goffs[k]):int(goffs[k + 1])]) for k in range(len(all_lens))]
+            want_crc = [c for per in every for c in per]
+            order = lzdist.stream_order(counts, world) if strong else np.arange(len(all_lens))
+            members = lzdist.reorder_payloads(gb.tobytes(), all_lens, order)
+            sizes = ([int(all_offs[i + 1] - all_offs[i]) for i in range(n_all)] if strong
+                     else [int(x) for x in np.tile(all_offs[1:] - all_offs[:-1], world)])
+            blob = lzdist.pack_container(props, members, sizes)
+            expect = n_all if strong else n_all * world
+            back = lzdist.unpack_container(blob)
+            gathered = {"bytes": int(g.numel()), "streams": len(back), "streams_expected": expect,
+                        "crc_match": got_crc == want_crc,
+                        "complete": len(back) == expect and got_crc == want_crc}
+            if strong and args.dump_container:
+                with open(args.dump_container, "wb") as f:
+                    f.write(blob)
+    return {"elapsed": elapsed, "timings": timings, "state": state, "host": host, "full": full, "offs": offs,
+            "n": n, "n_all": n_all, "size": size, "my_size": my_size, "comp_bytes": comp_bytes,
+            "roundtrip": roundtrip, "t_enc": state["t_enc"], "t_dec": state["t_dec"], "gathered": gathered,
+            "bufs": (d_in, d_comp, d_packs, d_dec)}
+
+
+def verify_parity(args, r, p, rank, world, dist, D, sample_idx=None):
+    """Oracle parity of the pass's streams (after the timed region). Returns (cpu_baseline
+    block or None, ok, streams checked)."""
+    cpu, ref = None, {}
+    n, offs, host = r["n"], r["offs"], r["host"]
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import oracle_ffi as orc
+    op = orc.params(p.dict_size, p.fb, p.mf, p.lc, p.lp, p.pb, p.eos)
+    chunks = [host[int(offs[i]):int(offs[i + 1])] for i in range(n)]
+    if rank == 0 and world == 1 and args.cpu_sample > 0 and sample_idx is None:
+        cpu, ref = cpu_baseline(orc, op, chunks, args)
+    if not args.no_verify:
+        if sample_idx is not None:
+            want = sample_idx
+        else:
+            want = range(n) if args.parity_streams < 0 else spread(n, args.parity_streams)
+        idx = [i for i in want if i not in ref]
+        if idx:   # not timed: the parity check of the streams the baseline sample did not cover
+            outs = orc.encode_many([chunks[i].tobytes() for i in idx], op, threads=orc.cpu_threads())
+            ref.update(zip(idx, outs))
+    ok, checked = True, 0
+    if ref:
+        host_pack = r["state"]["buf"][:r["comp_bytes"]].cpu().numpy()
+        pk = r["state"]["pk"]
+        for i, b in ref.items():
             checked += 1
-            if host_pack[int(pk[i]):int(pk[i + 1])].tobytes() != r:
-                parity_ok = False
-    ok = roundtrip and parity_ok and (checked > 0 or args.no_verify)
+            if host_pack[int(pk[i]):int(pk[i + 1])].tobytes() != b:
+                ok = False
+    ok = ok and r["roundtrip"] and (checked > 0 or args.no_verify)
+    if r["gathered"] is not None:
+        ok = ok and r["gathered"]["complete"]
     if dist:
-        flag = torch.tensor([1 if ok else 0, checked], device=dev, dtype=torch.int64)
+        flag = torch.tensor([1 if ok else 0, checked], device=D.dev, dtype=torch.int64)
         torch.distributed.all_reduce(flag[:1], op=torch.distributed.ReduceOp.MIN)
         torch.distributed.all_reduce(flag[1:], op=torch.distributed.ReduceOp.SUM)
         ok, checked = bool(flag[0].item()), int(flag[1].item())
+    return cpu, ok, checked, (orc, op)
+
+
+def main():
+    args = parse()
+    if args.emulate:
+        os.environ.setdefault("LZMA_AMD_LIB", SIMT_LIB)
+        lzma_amd.LIB_PATH = os.environ["LZMA_AMD_LIB"]
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = world > 1
+    D = Device(args.emulate, local)
+    if dist:
+        import torch.distributed as td
+        if args.emulate:
+            td.init_process_group("gloo")
+        else:
+            td.init_process_group("nccl", device_id=D.dev)
+        world = td.get_world_size()   # n_gpus comes from the process group
+        rank = td.get_rank()
+    dict_log = args.dict_log if args.dict_log is not None else (28 if args.data == "text" else 26)
+    p = lzma_amd.make_params(dict_size=1 << dict_log, fb=32, mf=1, lc=3, lp=0, pb=2)
+    ctx = lzma_amd.Context(D.index)
+    ctx.set_batch_bytes(args.batch_bytes)
+    ctx_dec = lzma_amd.Context(D.index)   # the decoder: its own context (device workspace) and HIP stream
+    ctxs = (ctx, ctx_dec, D.new_stream(), D.new_stream())
+
+    # ---- strong scaling: one --size buffer, streams dealt round-robin (value)
+    r = run_pass(args, D, p, ctxs, True, rank, world, dist)
+    cpu, ok, checked, (orc, op) = verify_parity(args, r, p, rank, world, dist, D)
+    weak = None
+    if dist and not args.no_weak:
+        del r["bufs"]
+        w = run_pass(args, D, p, ctxs, False, rank, world, dist)
+        wn = w["n"]
+        _, wok, wchecked, _ = verify_parity(args, w, p, rank, world, dist, D, sample_idx=spread(wn, 32))
+        weak = {"value": w["size"] * world * args.steps / w["elapsed"] / 1e6, "unit": "MB/s",
+                "ms_per_step": w["elapsed"] / args.steps * 1e3, "bytes_per_gpu": w["my_size"],
+                "streams_per_gpu": wn, "verified": wok, "parity_streams_checked": wchecked,
+                "gathered": w["gathered"],
+                "kernels_ms": {k: {"total_ms": v[0], "launches": v[1]} for k, v in w["timings"].items()}}
+        del w
 
     single = None
-    if rank == 0 and world == 1 and args.single_stream > 0:
-        single = single_stream(args, full, p, dev, st, orc if op is not None else None, op)
+    if rank == 0 and world == 1 and args.single_stream > 0 and not args.emulate:
+        single = single_stream(args, r["full"], p, D.dev, ctxs[2], orc, op)
 
-    total_bytes = (size if args.strong else size * world) * args.steps
-    value = total_bytes / elapsed / 1e6
+    elapsed, timings, size, my_size, n, n_all = r["elapsed"], r["timings"], r["size"], r["my_size"], r["n"], r["n_all"]
+    comp_bytes = r["comp_bytes"]
+    value = size * args.steps / elapsed / 1e6   # the one buffer's bytes per max-over-ranks step time
 
     # ---- roofline for the dominant kernel (HIP events on the launch stream)
     dom = max(timings.items(), key=lambda kv: kv[1][0]) if timings else ("none", (0.0, 1))
@@ -250,34 +384,45 @@ def main():
                 "avg_launch_ms": avg_s * 1e3, "launches_per_step": per_step_launches,
                 "alg_bytes_per_launch": alg, "issue": issue_bound(dname, wl, avg_s, my_size)}
 
-    t_enc, t_dec = state["t_enc"], state["t_dec"]
+    t_enc, t_dec = r["t_enc"], r["t_dec"]
+    ratio = comp_bytes / max(my_size, 1)
     if rank == 0:
         desc = "LzmaBench generator" if args.data == "bench" else "TEXT (enwik9-shaped) generator"
+        chunking = {"chunk_KiB": args.chunk >> 10, "ratio_chunked": ratio,
+                    "note": "configs 2/3 run as independent %d KiB streams (SURVEY 8(d) stream rule); the output "
+                            "is that many bytes larger than one whole-buffer stream would be" % (args.chunk >> 10)}
+        if single is not None:
+            chunking["ratio_one_stream"] = single["ratio"]
+            chunking["one_stream_bytes"] = single["bytes"]
+            chunking["extra_output_frac"] = ratio / single["ratio"] - 1 if single["ratio"] else None
         res = {
             "metric": "compress+decompress MB/s on 1 GB synthetic; bit-exact .lzma vs Java ref",
             "value": value, "unit": "MB/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
-            "scaling": "strong" if args.strong else "weak",
-            "vs_baseline": None, "dtype": "u8", "data": "synthetic (%s)" % desc,
-            "config": {"workload": "%s %d MiB %s as %d independent streams of %d KiB; dict 2^%d fb32 bt4 lc3 lp0 pb2 "
-                                   "(level-5 mapping); encode+pack+decode"
-                                   % (desc, size >> 20, "per job, dealt round-robin over the GPUs" if args.strong
-                                      else "per GPU", n_all, args.chunk >> 10, dict_log),
+            "scaling": "strong",
+            "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic (%s)%s" % (desc, "; CPU SIMT emulation, not a measurement" if args.emulate else ""),
+            "config": {"workload": "%s %d MiB as %d independent streams of %g KiB dealt round-robin over the GPUs; "
+                                   "dict 2^%d fb32 bt4 lc3 lp0 pb2 (level-5 mapping); encode+pack+decode"
+                                   % (desc, size >> 20, n_all, args.chunk / 1024, dict_log),
                        "bytes_per_gpu": my_size, "chunk": args.chunk, "streams_per_gpu": n,
-                       "parallelism": "independent streams, %d rank(s)%s" % (world, ", round-robin" if args.strong else "")},
-            "compress_MBps": my_size * world * args.steps / max(t_enc, 1e-9) / 1e6,
-            "decompress_MBps": my_size * world * args.steps / max(t_dec, 1e-9) / 1e6,
+                       "parallelism": "independent streams, %d rank(s), round-robin" % world},
+            "compress_MBps": size * args.steps / max(t_enc, 1e-9) / 1e6,
+            "decompress_MBps": size * args.steps / max(t_dec, 1e-9) / 1e6,
             "schedule": "sequential: each step's encode and decode back to back; compress/decompress MB/s are "
-                        "each phase's wall time",
-            "ratio": comp_bytes / max(my_size, 1), "verified": ok,
+                        "each phase's wall time (rank 0)",
+            "ratio": ratio, "chunking": chunking, "verified": ok,
             "verified_means": "every stream decodes to its input and every sampled stream's bytes equal the "
-                              "oracle's Encoder.Code restatement",
-            "parity_streams_checked": checked, "roundtrip_ok": roundtrip,
-            "gathered_bytes_rank0": state.get("gathered"),
+                              "oracle's Encoder.Code restatement%s" % (
+                                  "; rank 0's gathered container holds every stream" if dist else ""),
+            "parity_streams_checked": checked, "roundtrip_ok": r["roundtrip"],
+            "gathered": r["gathered"], "weak_scaling": weak,
             "kernels_ms": {k: {"total_ms": v[0], "launches": v[1]} for k, v in timings.items()},
             "roofline": roofline, "cpu_baseline": cpu, "single_stream": single,
         }
         print(json.dumps(res), flush=True)
+    if weak is not None:
+        ok = ok and weak["verified"]
     ctx.close()
     ctx_dec.close()
     if dist:
@@ -464,7 +609,8 @@ def single_stream(args, full, p, dev, st, orc, op):
     res = {"bytes": int(n), "dict_log": int(p.dict_size).bit_length() - 1, "gpu_compress_MBps": n / (t1 - t0) / 1e6,
            "gpu_decompress_MBps": n / (t2 - t1) / 1e6, "parse_ms": tm.get("enc_parse", (0.0, 0))[0],
            "parse_cycles_per_byte": tm.get("enc_parse", (0.0, 0))[0] / 1e3 * 2.4e9 / max(n, 1),
-           "ratio": len(enc) / max(n, 1), "roundtrip_ok": ok}
+           "ratio": len(enc) / max(n, 1), "roundtrip_ok": ok,
+           "projected_1GiB_encode_s": (1 << 30) / max(n / (t1 - t0), 1e-9)}
     if orc is not None:
         data = host.tobytes()
         c0 = time.perf_counter()

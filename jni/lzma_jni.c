@@ -17,6 +17,7 @@
  * the reference's Encoder/Decoder instances are single-threaded, and so is a context.
  */
 #include <jni.h>
+#include <limits.h>
 #include <pthread.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -42,6 +43,11 @@ JNIEXPORT jboolean JNICALL Java_SevenZip_Compression_LZMA_Native_init(JNIEnv *en
         int first = 0;
         while (!(m >> first & 1u)) first++;
         ok = lzma_ctx_create(first, &g_ctx) == LZMA_OK;
+        if (!ok) {   /* no half-initialised state: the next init starts over */
+            lzma_mctx_destroy(g_m);
+            g_m = NULL;
+            g_ctx = NULL;
+        }
     }
     pthread_mutex_unlock(&g_lock);
     return ok ? JNI_TRUE : JNI_FALSE;
@@ -69,6 +75,7 @@ JNIEXPORT jbyteArray JNICALL Java_SevenZip_Compression_LZMA_Native_encode(
         return NULL;
     }
     pthread_mutex_unlock(&g_lock);
+    if (len > (uint64_t)INT_MAX) { free(out); throw_io(env, "output longer than a Java array"); return NULL; }
     jbyteArray r = (*env)->NewByteArray(env, (jsize)len);
     if (r) (*env)->SetByteArrayRegion(env, r, 0, (jsize)len, (const jbyte *)out);
     free(out);
@@ -87,8 +94,11 @@ JNIEXPORT jbyteArray JNICALL Java_SevenZip_Compression_LZMA_Native_decode(
     uint8_t pr[5];
     (*env)->GetByteArrayRegion(env, props, 0, 5, (jbyte *)pr);
     const uint32_t dict = (uint32_t)pr[1] | ((uint32_t)pr[2] << 8) | ((uint32_t)pr[3] << 16) | ((uint32_t)pr[4] << 24);
-    /* a match may run past outSize (CopyBlock copies whole matches): 273 bytes of slack */
+    /* a match may run past outSize (CopyBlock copies whole matches): 273 bytes of slack;
+     * a Java array holds at most INT_MAX bytes, so the capacity never exceeds that */
+    if (out_size > (jlong)INT_MAX - 273) { throw_io(env, "output longer than a Java array"); return NULL; }
     uint64_t cap = out_size >= 0 ? (uint64_t)out_size + 273 : (uint64_t)n * 4 + 65536, len = 0;
+    if (cap > (uint64_t)INT_MAX) cap = (uint64_t)INT_MAX;
     for (;;) {
         uint8_t *dst = (uint8_t *)malloc(cap ? cap : 1);
         if (!dst) { throw_io(env, "out of memory"); return NULL; }
@@ -97,11 +107,17 @@ JNIEXPORT jbyteArray JNICALL Java_SevenZip_Compression_LZMA_Native_decode(
         pthread_mutex_lock(&g_lock);
         int rc = lzma_decode(g_ctx, pr, (const uint8_t *)src, (uint64_t)n, (int64_t)out_size, dst, cap, &len);
         (*env)->ReleasePrimitiveArrayCritical(env, in, src, JNI_ABORT);
-        if (rc == LZMA_E_OVERFLOW && out_size < 0 && cap < ((uint64_t)1 << 31)) {
+        if (rc == LZMA_E_OVERFLOW && out_size < 0 && cap < (uint64_t)INT_MAX) {
             pthread_mutex_unlock(&g_lock);
             free(dst);
-            cap *= 2;
+            cap = cap > (uint64_t)INT_MAX / 2 ? (uint64_t)INT_MAX : cap * 2;
             continue;
+        }
+        if (rc == LZMA_E_OVERFLOW && out_size < 0) {   /* the end marker lies beyond INT_MAX bytes */
+            pthread_mutex_unlock(&g_lock);
+            free(dst);
+            throw_io(env, "output longer than a Java array");
+            return NULL;
         }
         if (rc != LZMA_OK && rc != LZMA_E_DATA) {
             throw_io(env, lzma_last_error(g_ctx));
@@ -111,6 +127,7 @@ JNIEXPORT jbyteArray JNICALL Java_SevenZip_Compression_LZMA_Native_decode(
         }
         pthread_mutex_unlock(&g_lock);
         if (rc == LZMA_E_DATA) len = lzma_visible_on_error(dict, len);
+        if (len > (uint64_t)INT_MAX) { free(dst); throw_io(env, "output longer than a Java array"); return NULL; }
         jint st = rc;
         (*env)->SetIntArrayRegion(env, status, 0, 1, &st);
         jbyteArray r = (*env)->NewByteArray(env, (jsize)len);

@@ -443,9 +443,15 @@ __global__ void __launch_bounds__(kWave) dec_kernel(DecArgs a) {
     d.lit = (uint16_t*)(a.scratch + (size_t)blockIdx.x * a.scratch_stride);
     // one workgroup per stream; per-stream values are wave-uniform (readfirstlane keeps them scalar)
     const int s = __builtin_amdgcn_readfirstlane((int)a.order[blockIdx.x]);
+    if (s < 0 || s >= a.nstreams) return;   // a corrupt order entry: touch nothing (the host checked the order it wrote)
     const uint64_t i0 = dec_uni64(a.in_offs[s]), o0 = dec_uni64(a.out_offs[s]);
+    const uint64_t i1 = dec_uni64(a.in_offs[s + 1]), o1 = dec_uni64(a.out_offs[s + 1]);
+    if (i1 < i0 || o1 < o0) {   // offsets the host validated, changed under the kernel: report, do not fault
+        if (d.lane == 0) { a.out_lens[s] = 0; a.status[s] = LZMA_E_INTERNAL; }
+        return;
+    }
     d.in = a.in + i0;
-    const uint64_t n_in = dec_uni64(a.in_offs[s + 1]) - i0, cap = dec_uni64(a.out_offs[s + 1]) - o0;
+    const uint64_t n_in = i1 - i0, cap = o1 - o0;
     d.n_in = n_in > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)n_in;   // the host rejects inputs >= 4 GiB
     d.out = a.out + o0;
     d.cap = cap > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)cap;

@@ -1525,6 +1525,11 @@ __global__ void __launch_bounds__(kWave, 4) enc_kernel(EncArgs a) {
     // wave-uniform by construction; readfirstlane keeps them (and the buffer
     // descriptor built from them) in SGPRs, so buffer loads need no waterfall loop
     const int s = __builtin_amdgcn_readfirstlane((int)a.order[blockIdx.x]);
+    if (s < 0 || s >= a.nstreams) return;   // a corrupt order entry: touch nothing (the host checked the order it wrote)
+    if (uni64(a.offs[s + 1]) < uni64(a.offs[s]) || uni64(a.rec_offs[s + 1]) < uni64(a.rec_offs[s])) {
+        if (e.lane == 0) { a.rec_lens[s] = 0; a.out_lens[s] = 9ull << 32; a.status[s] = LZMA_E_INTERNAL; }
+        return;
+    }
     e.gbase = uni64(a.offs[s]);
     e.n = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(uni64(a.offs[s + 1]) - e.gbase));
     e.in = a.in + e.gbase;

@@ -376,10 +376,15 @@ __global__ void __launch_bounds__(64) LZG_WALK_ATTR mf_walk_kernel(const uint8_t
                                                      int* __restrict__ err) {
     using PP = PairPack<PairT>;
     uint32_t c;
+    // The walk trusts nothing it did not compute itself: a chain index, a chain's
+    // extent, its stream and every member's position are range-checked, and a bad
+    // one ends the lane with err = 4 (LZMA_E_INTERNAL on the host) instead of a
+    // fault or a member loop that never ends.
     if (blockIdx.x < long_blocks) {   // the long chains, longest first, dealt over the XCDs in dispatch order
         const uint64_t li = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
         if (li >= n_long) return;
         c = long_list[li];
+        if ((uint64_t)c >= a.total) { *err = 4; return; }
     } else {
         // XCD-aware mapping: the dispatcher places block b on XCD b % 8, so XCD x takes
         // the x-th eighth of the (stream-ordered) chain list and its L2 serves a few
@@ -390,13 +395,16 @@ __global__ void __launch_bounds__(64) LZG_WALK_ATTR mf_walk_kernel(const uint8_t
         const uint64_t ci = blk * blockDim.x + threadIdx.x;
         if (ci >= nchains) return;
         c = chain_order[ci];
+        if ((uint64_t)c >= a.total) { *err = 4; return; }
         if (chain_len[c] >= min_len) return;   // walked by the front blocks
     }
     uint64_t start = chain_start[c], end = start + chain_len[c];
     if (start == end) return;   // a stream's sentinel run
+    if (end > a.total || end < start) { *err = 4; return; }
     if (end - start < a.walk_lo || end - start > a.walk_hi) return;   // timing experiment only (LZG_WALK_ONLY)
     uint64_t key = keys4[start];
     int s = (int)(key >> (BT4 ? a.hash_bits : 16));
+    if (key == kSentinel || s < 0 || s >= a.nstreams) { *err = 4; return; }
     uint64_t base = offs[s], n = offs[s + 1] - base;
     const uint8_t* sb = in + base;          // stream bytes, 0-based
     const uint32_t fb = a.fb, cut = a.cut_value;
@@ -433,6 +441,7 @@ __global__ void __launch_bounds__(64) LZG_WALK_ATTR mf_walk_kernel(const uint8_t
     uint64_t c0 = load8(sb + (g - base)), c1 = load8(sb + (g - base) + 8);   // this member's prefix
     cand_bytes(pv2, pv3, b2, b3);
     for (uint64_t i = start; i < end; i++) {
+        if (g - base >= n) { *err = 4; return; }   // a member outside its chain's stream
         const uint64_t g3 = i + 3 < end ? vals4[i + 3] : 0;
         uint32_t pv2nn = kNoPos, pv3nn = kNoPos, b2n = 0, b3n = 0;
         uint64_t c0n = 0, c1n = 0;
@@ -593,6 +602,7 @@ int run_match_finder(Ctx* ctx, const Derived& d, const uint8_t* in, const uint64
     a.fb = d.fb; a.min_match_check = d.min_match_check; a.hash_mask = d.hash_mask; a.hash_bits = d.hash_bits;
     a.cut_value = d.cut_value; a.cyc_size = d.cyc_size; a.direct_bytes = d.direct_bytes;
     a.walk_lo = 0; a.walk_hi = 0xFFFFFFFFu;
+    a.total = total; a.nstreams = nstreams;
     if (const char* e = getenv("LZG_WALK_ONLY")) {   // "lo,hi": a timing experiment; the output is incomplete
         unsigned lo = 0, hi = 0xFFFFFFFFu;
         if (sscanf(e, "%u,%u", &lo, &hi) >= 1) { a.walk_lo = lo; a.walk_hi = hi; }
@@ -685,6 +695,7 @@ int run_match_finder(Ctx* ctx, const Derived& d, const uint8_t* in, const uint64
     hipMemcpyAsync(p_err, w.err, sizeof(int), hipMemcpyDeviceToHost, st);
     if (hipStreamSynchronize(st) != hipSuccess) return ctx->fail(LZMA_E_DEVICE, "mf_walk: %s", hipGetErrorString(hipGetLastError()));
     if (*p_err == 3) return ctx->fail(LZMA_E_INTERNAL, "mf_walk: a tree link outside its bucket");
+    if (*p_err == 4) return ctx->fail(LZMA_E_INTERNAL, "mf_walk: a chain list entry out of range (index, extent, stream or member)");
     if (*p_err) return LZMA_E_OVERFLOW;   // caller grows the overflow pool and retries
     return LZMA_OK;
 }

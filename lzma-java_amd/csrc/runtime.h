@@ -30,6 +30,8 @@ struct MfArgs {
     uint32_t *vals, *prev2, *prev3;
     v4u32* mrec;                  // per-position match-list records (lzma_common.h store_rec)
     uint32_t walk_lo, walk_hi;    // experiment hook (LZG_WALK_ONLY): walk only chains of length in [lo, hi]
+    uint64_t total;               // positions of the pass (every chain, sorted index and position is below it)
+    int nstreams;
 };
 
 struct MfBuffers {

@@ -9,8 +9,10 @@
 // would compute returns LZMA_E_NODEVICE.
 #include <algorithm>
 #include <cstring>
+#include <mutex>
 #include <new>
 #include <numeric>
+#include <set>
 #include <vector>
 
 #include "lzma_common.h"
@@ -33,6 +35,11 @@ __global__ void pack_kernel(const uint8_t* __restrict__ src, const uint64_t* __r
 }
 
 static bool ok_ctx(const Ctx* c) { return c && c->magic == kCtxMagic; }
+
+// Live contexts: lzma_ctx_destroy clears every parse fence that names the context
+// being destroyed, so a fence never points at freed memory.
+static std::mutex g_ctx_lock;
+static std::set<Ctx*> g_live_ctx;
 
 static int check_device(Ctx* ctx) {
     int n = 0;
@@ -271,7 +278,8 @@ static int encode_pass(Ctx* ctx, const Derived& d, const uint8_t* d_in, const ui
 #endif
         // a pipelined caller's decoder (another context) may still hold CUs: the
         // parser needs every stream resident from its start, so it waits for it
-        if (ctx->fence && ctx->fence->dec_pending) HIPCHK(hipStreamWaitEvent(st, ctx->fence->dec_done, 0));
+        if (ctx->fence && ok_ctx(ctx->fence) && ctx->fence->dec_pending)
+            HIPCHK(hipStreamWaitEvent(st, ctx->fence->dec_done, 0));
         if ((rc = launch_encoder(ctx, a, wide, grid, st))) return rc;
         LZG_TRACE(ctx, st, "enc_parse done");
         watch.stop();
@@ -518,12 +526,22 @@ int lzma_ctx_create(int device, lzma_ctx** out) {
     lzma_ctx* c = new (std::nothrow) lzma_ctx();
     if (!c) return LZMA_E_NOMEM;
     c->device = device;
+    {
+        std::lock_guard<std::mutex> g(g_ctx_lock);
+        g_live_ctx.insert(c);
+    }
     *out = c;
     return LZMA_OK;
 }
 
 void lzma_ctx_destroy(lzma_ctx* ctx) {
     if (!ok_ctx(ctx)) return;
+    {
+        std::lock_guard<std::mutex> g(g_ctx_lock);
+        g_live_ctx.erase(ctx);
+        for (Ctx* o : g_live_ctx)
+            if (o->fence == ctx) o->fence = nullptr;   // an encoder fenced on this decoder: no fence any more
+    }
     hipSetDevice(ctx->device);
     ctx->resolve_timings();
     for (auto e : ctx->free_events) hipEventDestroy(e);
@@ -587,6 +605,9 @@ int lzma_pack_dev(lzma_ctx* ctx, const uint8_t* d_src, const uint64_t* h_src_off
     if (!ok_ctx(ctx) || !h_src_offs || !h_lens || !h_dst_offs || nstreams < 0) return LZMA_E_PARAM;
     if (check_device(ctx)) return LZMA_E_NODEVICE;
     if (nstreams == 0) return LZMA_OK;
+    // the pack carves the front of the arena, where a decode in flight keeps its offsets
+    // and results (decode_enqueue), and may grow (reallocate) it
+    if (ctx->dec_pending) return ctx->fail(LZMA_E_PARAM, "an asynchronous decode is in flight: lzma_dec_batch_dev_wait first");
     hipSetDevice(ctx->device);
     hipStream_t st = (hipStream_t)hip_stream;
     for (int i = 0; i < nstreams; i++)

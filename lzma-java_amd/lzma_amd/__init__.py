@@ -562,12 +562,14 @@ class Decoder:
         ctx = self._ctx or default_context()
         cap = outSize if outSize >= 0 else max(64 * len(data), 1 << 16)
         while True:
-            st, out = ctx.decode_batch([data], self._props, [outSize], caps=[cap + 64])[0]
+            # the loop of Decoder.java:219 stops at outSize only between symbols: a final
+            # match may run up to kMatchMaxLen (273) bytes past it and is written whole
+            st, out = ctx.decode_batch([data], self._props, [outSize], caps=[cap + 273])[0]
             if st == LZMA_E_OVERFLOW and outSize < 0:
                 cap *= 4
                 continue
             break
-        if st != LZMA_OK:
+        if st == LZMA_E_DATA:
             # Code returns false with only the whole windows OutWindow flushed so far
             # written (OutWindow.java:63-73; window = max(dict, 4096), Decoder.java:167)
             dict_size = int.from_bytes(self._props[1:5], "little")

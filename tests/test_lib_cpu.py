@@ -180,3 +180,19 @@ def test_visible_on_error_is_whole_windows(dict_size, n, exp):
     # Decoder.Code returning false has written only OutWindow's whole-window flushes
     # (OutWindow.java:63-73), window = max(dict, 4096) (Decoder.java:166-167)
     assert lzma_amd.visible_on_error(dict_size, n) == exp
+
+
+def test_jni_shim_compiles():
+    """Compile check of the JNI shim (jni/lzma_jni.c) against a minimal stand-in
+    jni.h (tests/jni_stub/): there is no JDK in this container or on the GPU box,
+    so this catches C errors before a maintainer with a JDK builds jni/Makefile.
+    It is NOT parity evidence: the shim is never linked or called here."""
+    import shutil
+    import subprocess
+    cc = shutil.which("gcc") or shutil.which("cc")
+    if cc is None:
+        pytest.skip("no C compiler")
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    subprocess.check_call([cc, "-fsyntax-only", "-std=c11", "-Wall", "-Wextra", "-Werror",
+                           "-I" + os.path.join(repo, "tests", "jni_stub"), "-I" + os.path.join(repo, "include"),
+                           os.path.join(repo, "jni", "lzma_jni.c")])
