@@ -129,7 +129,8 @@ int lzma_dec_batch_dev(lzma_ctx *ctx, const uint8_t props[5],
  * once (the host arrays are copied into the context's pinned staging first);
  * _wait blocks until it is done and writes h_out_lens / h_status (either may
  * be NULL). One decode may be in flight per context, and the context runs
- * nothing else until _wait. */
+ * nothing else until _wait (every other entry point returns LZMA_E_PARAM).
+ * Another context may encode meanwhile, on another HIP stream. */
 int lzma_dec_batch_dev_async(lzma_ctx *ctx, const uint8_t props[5],
                              const uint8_t *d_in, const uint64_t *h_in_offs, int nstreams,
                              const int64_t *h_out_sizes, uint8_t *d_out, const uint64_t *h_out_offs,
@@ -138,7 +139,7 @@ int lzma_dec_batch_dev_wait(lzma_ctx *ctx, uint64_t *h_out_lens, int32_t *h_stat
 /* Encode passes on ctx launch their parser only after dec_ctx's decode in
  * flight (if any) has finished: the parser wants every stream resident from
  * its start, so a concurrent decode may share the match finder's time but not
- * the parse's. NULL clears the fence. */
+ * the parse's. NULL clears the fence; destroying dec_ctx clears it too. */
 int lzma_ctx_set_parse_fence(lzma_ctx *ctx, const lzma_ctx *dec_ctx);
 int lzma_dec_batch(lzma_ctx *ctx, const uint8_t props[5],
                    const uint8_t *in, const uint64_t *in_offs, int nstreams,

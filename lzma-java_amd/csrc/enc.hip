@@ -47,10 +47,11 @@ constexpr int kMdCap = kMatchMaxLen + 1;
 constexpr int kRing = 32;           // match-info prefetch window (positions)
 constexpr int kGW = 64;             // gather window: offsets -1 .. kGW-2 around the current position
 constexpr int kGI = kGW / kWave;    // gather iterations per side (1 on hardware)
-constexpr int kSides = 7;           // cur, rep0..rep3, pair0, pair1
+constexpr int kSides = 7;           // gathered sides: cur, rep0..rep3, pair0, pair1 (only cur's bytes go to LDS)
+constexpr int kWinBytes = 2 * kNumFullDistances;   // LDS: the cur side's kGW bytes, aliased by tempPrices
 constexpr int kRbuf = 128;          // coder-record staging ring (records, power of two; halves of 64 go to HBM)
 constexpr int kLitSlots = (8 + kWave - 1) / kWave;   // literal bits per lane (1 on hardware)
-static_assert(kSides * kGW >= kNumFullDistances * 2, "tempPrices alias the gather window");
+static_assert(kWinBytes >= kGW, "the gather window holds the cur side");
 
 #define FI __device__ __forceinline__
 // Lanes of one wavefront exchange data through LDS. The hardware runs one
@@ -144,8 +145,8 @@ struct Enc {
     uint16_t* dp;             // _distancesPrices [512]
     uint32_t* ap;             // _alignPrices [16]
     uint16_t* tp;             // tempPrices [128]
-    uint16_t* md_len;
-    uint32_t* md_dist;
+    const PairT* mdp;         // the current position's pairs (packed): its ring slot, or md_buf
+    PairT* md_buf;            // a copy when the list is longer than the inline pairs or is clamped
     uint32_t* ring_info;      // [kRing]
     PairT* ring_pairs;        // [kRing * kInlinePairs]
     uint32_t* o_price;        // _optimum SoA, [kOptLds] each (+ the sink entry, + kFarEntry)
@@ -156,7 +157,7 @@ struct Enc {
     uint32_t* o_backs;        // [4][kOptLds]
     uint32_t* o_bytes;        // [kOptLds] cur byte | match byte << 8 | previous byte << 16 of each parsed
                               // position, so the coder needs no HBM byte loads (RING: | state << 24)
-    uint8_t* win;             // gather window [kSides][kGW]: cur side, reps 0-3, pairs 0-1
+    uint8_t* win;             // gather window: the cur side's bytes at offsets -1 .. kGW - 2
     uint16_t* rbuf;           // coder-record staging ring [kRbuf]
     __amdgpu_buffer_rsrc_t spill;   // _optimum slots >= kOptLds in HBM (9 fields x kNumOpts dwords)
     // ---- parameters
@@ -191,6 +192,7 @@ struct Enc {
     // ---- per-position gather (see gather()): p = current position, equality masks per side
     uint32_t gp;
     uint64_t gm0, gm1, gm2, gm3, gmp0, gmp1;
+    uint32_t g_prev, g_cur, g_mb;   // bytes at p - 1 and p, and at p - rep0 - 1 (the match byte), from the gather
 #ifdef LZG_PROF
     uint64_t prof[kProfSlots];
 #endif
@@ -264,7 +266,10 @@ struct Enc {
         LANE_FOR(uint32_t, k, 0u, 5u) sstore(5 + k, i, k < 4 ? o_backs[k * kOptLds + r] : o_bytes[r]);
     }
     // the gather window's bytes of the current position (see gather())
-    FI uint32_t win_bytes() const { return (uint32_t)win[1] | ((uint32_t)win[kGW + 1] << 8) | ((uint32_t)win[0] << 16); }
+    // pair k of the current position's match list
+    FI uint32_t md_l(uint32_t k) const { return PP::len(mdp[k]); }
+    FI uint32_t md_d(uint32_t k) const { return PP::dist(mdp[k]); }
+    FI uint32_t win_bytes() const { return g_cur | (g_mb << 8) | (g_prev << 16); }
     template <bool F = false> FI uint32_t pos_prev(uint32_t i) const { return pp_at<F>(i) & 0xFFFFu; }
     template <bool F = false> FI uint32_t pos_prev2(uint32_t i) const { return pp_at<F>(i) >> 16; }
     // after lanes wrote slots up to `hi`, make them visible to every lane
@@ -374,7 +379,7 @@ struct Enc {
     FI void gather(bool with_pairs) {
         gp = mfpos - 1;
         const uint32_t d0 = rp0 + 1, d1 = rp1 + 1, d2 = rp2 + 1, d3 = rp3 + 1;
-        const uint32_t e0 = num_pairs > 0 ? md_dist[0] + 1 : d0, e1 = num_pairs > 1 ? md_dist[1] + 1 : d0;
+        const uint32_t e0 = num_pairs > 0 ? md_d(0) + 1 : d0, e1 = num_pairs > 1 ? md_d(1) + 1 : d0;
         uint32_t va[kGI], v0[kGI], v1[kGI], v2[kGI], v3[kGI], w0[kGI], w1[kGI];
 #pragma unroll
         for (int it = 0; it < kGI; it++) {
@@ -392,25 +397,29 @@ struct Enc {
             gm1 |= (uint64_t)__ballot(va[it] == v1[it]) << sh;
             gm2 |= (uint64_t)__ballot(va[it] == v2[it]) << sh;
             gm3 |= (uint64_t)__ballot(va[it] == v3[it]) << sh;
-            win[k] = (uint8_t)va[it];
-            win[1 * kGW + k] = (uint8_t)v0[it]; win[2 * kGW + k] = (uint8_t)v1[it];
-            win[3 * kGW + k] = (uint8_t)v2[it]; win[4 * kGW + k] = (uint8_t)v3[it];
+            win[k] = (uint8_t)va[it];   // the cur side only: the other sides' bytes are read (rarely, by a
+                                         // two-step candidate's literal) straight from the stream
             if (with_pairs) {
                 gmp0 |= (uint64_t)__ballot(va[it] == w0[it]) << sh;
                 gmp1 |= (uint64_t)__ballot(va[it] == w1[it]) << sh;
-                win[5 * kGW + k] = (uint8_t)w0[it]; win[6 * kGW + k] = (uint8_t)w1[it];
             }
         }
+        // the three bytes every position step reads, straight from the loaded registers
+        // (offsets -1 and 0 are window entries 0 and 1): no LDS round trip on the chain
+        g_prev = lane_value(va, 0);
+        g_cur = lane_value(va, 1);
+        g_mb = lane_value(v0, 1);
         LANE_FENCE();
     }
     // byte at p + o on the cur side
     FI uint32_t a_byte(int32_t o) const {
         return (o >= -1 && o <= kGW - 2) ? (uint32_t)win[o + 1] : in_byte(gp + (uint32_t)o);
     }
-    // byte at p + o - dist - 1 (side 1..6 = rep0..3, pair0..1; side < 0: not gathered)
+    // byte at p + o - dist - 1 (side 1..6 = rep0..3, pair0..1; side < 0: not gathered); only a
+    // two-step candidate's literal reads one (a few percent of the positions): from the stream
     FI uint32_t b_byte(int side, uint32_t dist, int32_t o) const {
-        return (side > 0 && o >= -1 && o <= kGW - 2) ? (uint32_t)win[side * kGW + o + 1]
-                                                       : in_byte(gp + (uint32_t)o - dist - 1);
+        (void)side;
+        return in_byte(gp + (uint32_t)o - dist - 1);
     }
     // InWindow.GetMatchLen(index = o - 1, dist, limit) from the side's mask; the
     // part of the compare beyond the window continues with match_len.
@@ -557,7 +566,10 @@ struct Enc {
             else { q_bit(q, L + LEN_CHOICE + 1, 1); q_bt(q, L + E_HIGH, 8, sym - kNumMidLenSymbols); }
         }
     }
-    FI void q_run(const Q& q) {
+    // has_lit (wave-uniform): the symbol codes a literal. Only then do the lanes load and
+    // store the literal coders (HBM): a global store of the other symbols would make the
+    // next load on the chain wait for it (vmcnt counts stores and loads alike).
+    FI void q_run(const Q& q, bool has_lit) {
         // branch-free: every lane loads and stores; lanes whose slot is not of a kind use the
         // sink entry past that table (lit: nlit, probs: E_COUNT, dmp: E_PSLOT, rbuf: kRbuf)
         const uint32_t nlit = 0x300u << (lc + lp);
@@ -565,7 +577,7 @@ struct Enc {
 #pragma unroll
         for (int t = 0; t < kQS; t++) {
             const bool isl = q.kind[t] == QK_LIT, isp = q.kind[t] == QK_PROB;
-            const uint32_t lv = lit[isl ? q.idx[t] : nlit];
+            const uint32_t lv = has_lit ? (uint32_t)lit[isl ? q.idx[t] : nlit] : 0u;
             const uint32_t pv = probs[isp ? q.idx[t] : (uint32_t)E_COUNT];
             pr[t] = isl ? lv : (isp ? pv : 0u);
         }
@@ -579,9 +591,9 @@ struct Enc {
             const uint32_t p = pr[t];
             const uint16_t np = (uint16_t)(q.bit[t] ? p - (p >> kNumMoveBits) : p + ((kBitModelTotal - p) >> kNumMoveBits));
 #ifdef LZG_ABL_LITSTORE
-            lit[nlit] = np;   // ablation: literal models never adapt
+            if (has_lit) lit[nlit] = np;   // ablation: literal models never adapt
 #else
-            lit[isl ? q.idx[t] : nlit] = np;
+            if (has_lit) lit[isl ? q.idx[t] : nlit] = np;
 #endif
             probs[isp ? q.idx[t] : (uint32_t)E_COUNT] = np;
             dmp[(isp && q.idx[t] < (uint32_t)E_PSLOT) ? q.idx[t] : (uint32_t)E_PSLOT] = price0(np) | (price1(np) << 16);
@@ -663,22 +675,16 @@ struct Enc {
         uint32_t slot = q - ring_base;
         uint32_t info = ring_info[slot];
         uint32_t cnt = info & 0xFFFFu, ml = info >> 16;
-        if (cnt <= (uint32_t)kInlinePairs) {   // LDS only (no wait on outstanding HBM operations)
-            LANE_FOR(uint32_t, k, 0u, cnt) {
-                const PairT pr = ring_pairs[slot * kInlinePairs + k];
-                md_len[k] = (uint16_t)PP::len(pr);
-                md_dist[k] = PP::dist(pr);
-            }
+        if (cnt <= (uint32_t)kInlinePairs) {   // read in place from the ring: no copy, no LDS round trip
+            mdp = ring_pairs + slot * kInlinePairs;
         } else {
             PCOUNT(PF_NOVF);
-            LANE_FOR(uint32_t, k, 0u, cnt) {
-                PairT pr = k < (uint32_t)kInlinePairs ? ring_pairs[slot * kInlinePairs + k]
-                                                      : ovf[(uint64_t)ovf_off[gbase + q] * ovf_stride(fb) + k - kInlinePairs];
-                md_len[k] = (uint16_t)PP::len(pr);
-                md_dist[k] = PP::dist(pr);
-            }
+            LANE_FOR(uint32_t, k, 0u, cnt)
+                md_buf[k] = k < (uint32_t)kInlinePairs ? ring_pairs[slot * kInlinePairs + k]
+                                                       : ovf[(uint64_t)ovf_off[gbase + q] * ovf_stride(fb) + k - kInlinePairs];
+            LANE_FENCE();
+            mdp = md_buf;
         }
-        LANE_FENCE();
         num_pairs = cnt;
         mfpos++;
         additional_offset++;
@@ -833,8 +839,8 @@ struct Enc {
                 // the pair of length l: the first with md_len >= l (lengths increase), i.e. the count of
                 // shorter ones among the first npairs - 1 -- a uniform loop instead of a per-lane while
                 uint32_t k = 0;
-                for (uint32_t kk = 0; kk + 1 < npairs; kk++) k += l > md_len[kk] ? 1u : 0u;
-                const uint32_t distance = md_dist[k];
+                for (uint32_t kk = 0; kk + 1 < npairs; kk++) k += l > md_l(kk) ? 1u : 0u;
+                const uint32_t distance = md_d(k);
                 const uint32_t s = ok ? l : (uint32_t)kOptLds;
                 const uint32_t cl = normal_match_price + pos_len_price(distance, ok ? l : (uint32_t)kMatchMinLen, pos_state);
                 const uint32_t op = o_price[s], opp = o_pp[s], ofs = o_fs[s];
@@ -849,8 +855,8 @@ struct Enc {
         }
         LANE_FOR(uint32_t, l, lstart, len_main + 1) {
             uint32_t k = 0;
-            while (k + 1 < npairs && l > md_len[k]) k++;
-            uint32_t distance = md_dist[k];
+            while (k + 1 < npairs && l > md_l(k)) k++;
+            uint32_t distance = md_d(k);
             uint32_t cl = normal_match_price + pos_len_price(distance, l, pos_state);
             if (cl < price_at<F>(l)) {
                 set_price<F>(l, cl);
@@ -972,10 +978,11 @@ struct Enc {
         uint32_t num_avail = avail() + 1;
         if (num_avail < 2) { *back_res = -1; LANE_FENCE(); return 1; }
         if (num_avail > (uint32_t)kMatchMaxLen) num_avail = kMatchMaxLen;
-        uint32_t rl0 = glen(gm0, rp0, 0, kMatchMaxLen);
-        uint32_t rl1 = glen(gm1, rp1, 0, kMatchMaxLen);
-        uint32_t rl2 = glen(gm2, rp2, 0, kMatchMaxLen);
-        uint32_t rl3 = glen(gm3, rp3, 0, kMatchMaxLen);
+        // a rep whose first byte differs (mask bit 1 clear) has length 0: no glen
+        uint32_t rl0 = (gm0 & 2u) ? glen(gm0, rp0, 0, kMatchMaxLen) : 0u;
+        uint32_t rl1 = (gm1 & 2u) ? glen(gm1, rp1, 0, kMatchMaxLen) : 0u;
+        uint32_t rl2 = (gm2 & 2u) ? glen(gm2, rp2, 0, kMatchMaxLen) : 0u;
+        uint32_t rl3 = (gm3 & 2u) ? glen(gm3, rp3, 0, kMatchMaxLen) : 0u;
         PEND(PF_REPLEN, t0);
         uint32_t rep_max = 0, rl_max = rl0;
         if (rl1 > rl_max) { rep_max = 1; rl_max = rl1; }
@@ -987,19 +994,19 @@ struct Enc {
             return rl_max;
         }
         if (len_main >= fb) {
-            *back_res = (int32_t)(md_dist[npairs - 1] + kNumRepDistances);
+            *back_res = (int32_t)(md_d(npairs - 1) + kNumRepDistances);
             move_pos(len_main - 1);
             return len_main;
         }
-        uint32_t cur_byte = a_byte(0);
-        uint32_t match_byte = b_byte(1, rp0, 0);   // rp0 == rd0 here
+        uint32_t cur_byte = g_cur;
+        uint32_t match_byte = g_mb;   // rp0 == rd0 here
         if (len_main < 2 && cur_byte != match_byte && rl_max < 2) { *back_res = -1; return 1; }
 
         if (!RING) set_fs<true>(0, (fs_at<true>(0) & 0xFu) | (state << 4));
         uint32_t pos_state = position & ps_mask;
         PBEGIN(t1);
         uint32_t p1 = dm0(E_IS_MATCH + (state << PBS) + pos_state) +
-                      lit_price(lit_coder(position, a_byte(-1)), !st_is_char(state), match_byte, cur_byte);
+                      lit_price(lit_coder(position, g_prev), !st_is_char(state), match_byte, cur_byte);
         PEND(PF_LIT, t1);
         uint32_t match_price = dm1(E_IS_MATCH + (state << PBS) + pos_state);
         uint32_t rep_match_price = match_price + dm1(E_IS_REP + state);
@@ -1100,23 +1107,25 @@ struct Enc {
         set_back<FA>(cur, 0, rp0); set_back<FA>(cur, 1, rp1); set_back<FA>(cur, 2, rp2); set_back<FA>(cur, 3, rp3);
         uint32_t cur_price = price_at<FA>(cur);
         pos_state = position & ps_mask;
+        // cur + 1's slot: nothing before its literal / short-rep update below writes it, so its
+        // reads are issued before the gather and complete under the gather's memory round trip
+        uint32_t nx = cur + 1;
+        uint32_t nx_price = price_at<FA>(nx);
+        uint32_t nx_pp = pp_at<FA>(nx);
+        int32_t nx_bp = bp_at<FA>(nx);
         PEND(PF_STATE, ts);
         PBEGIN(tg);
         gather(true);
         set_bytes<FA>(cur, win_bytes() | (RING ? st << 24 : 0u));
         PEND(PF_REPLEN, tg);
-        cur_byte = a_byte(0);
-        match_byte = b_byte(1, rp0, 0);
+        cur_byte = g_cur;
+        match_byte = g_mb;
         PBEGIN(tl);
         cur_and1 = cur_price + dm0(E_IS_MATCH + (st << PBS) + pos_state) +
-                            lit_price(lit_coder(position, a_byte(-1)), !st_is_char(st), match_byte, cur_byte);
+                            lit_price(lit_coder(position, g_prev), !st_is_char(st), match_byte, cur_byte);
         PEND(PF_LIT, tl);
         PBEGIN(tn);
-        uint32_t nx = cur + 1;
         bool next_is_char = false;
-        uint32_t nx_price = price_at<FA>(nx);
-        uint32_t nx_pp = pp_at<FA>(nx);
-        int32_t nx_bp = bp_at<FA>(nx);
         if (cur_and1 < nx_price) {
             nx_price = cur_and1; nx_pp = (nx_pp & 0xFFFF0000u) | cur; nx_bp = -1;
             set_price<FA>(nx, nx_price); set_pp<FA>(nx, nx_pp); set_bp<FA>(nx, -1); set_fs<FA>(nx, fs_at<FA>(nx) & ~1u);
@@ -1179,7 +1188,8 @@ struct Enc {
             uint32_t num_avail = num_avail_full;
             if (num_avail < 2) continue;
             if (num_avail > fb) num_avail = fb;
-            if (!next_is_char && match_byte != cur_byte) {   // literal + rep0
+            // literal + rep0: lenTest2 >= 2 needs the bytes at offsets 1 and 2 equal (mask bits 2, 3)
+            if (!next_is_char && match_byte != cur_byte && (gm0 & 0xCu) == 0xCu) {
                 uint32_t t = num_avail_full - 1 < fb ? num_avail_full - 1 : fb;
                 PBEGIN(t2a);
                 uint32_t lt2 = glen(gm0, rp0, 1, (int32_t)t);
@@ -1200,6 +1210,8 @@ struct Enc {
             for (uint32_t ri = 0; ri < (uint32_t)kNumRepDistances; ri++) {
                 uint32_t rdist = sel4(ri, rp0, rp1, rp2, rp3);
                 const uint64_t gmr = ri == 0 ? gm0 : (ri == 1 ? gm1 : (ri == 2 ? gm2 : gm3));
+                // lenTest >= 2 needs offsets 0 and 1 equal (mask bits 1, 2): most reps stop here
+                if ((gmr & 6u) != 6u) continue;
                 PBEGIN(tr);
                 uint32_t lt = glen(gmr, rdist, 0, (int32_t)num_avail);
                 PEND(PF_REPLEN, tr);
@@ -1209,7 +1221,8 @@ struct Enc {
                 relax_rep(cur, 2, lt, rep_match_price + pure_rep_price(ri, st, pos_state), pos_state, cur, ri);
                 PEND(PF_RELAX, trr);
                 if (ri == 0) start_len = lt + 1;
-                if (lt < num_avail_full) {
+                // the two-step lenTest2 >= 2 needs offsets lt + 1 and lt + 2 equal (mask bits lt + 2, lt + 3)
+                if (lt < num_avail_full && (lt + 3 >= 64u || ((gmr >> (lt + 2)) & 3u) == 3u)) {
                     uint32_t t = num_avail_full - 1 - lt;
                     if (t > fb) t = fb;
                     PBEGIN(tq);
@@ -1236,10 +1249,13 @@ struct Enc {
             if (new_len > num_avail) {
                 new_len = num_avail;
                 uint32_t np0 = npairs;
-                for (npairs = 0; npairs + 1 < np0 && new_len > md_len[npairs]; npairs++) {}
-                md_len[npairs] = (uint16_t)new_len;
-                npairs++;
+                for (npairs = 0; npairs + 1 < np0 && new_len > md_l(npairs); npairs++) {}
+                // the clamped list goes to md_buf (the ring slot stays the match finder's)
+                LANE_FOR(uint32_t, k, 0u, npairs + 1)
+                    md_buf[k] = k < npairs ? mdp[k] : PP::pack(new_len, md_d(npairs));
                 LANE_FENCE();
+                mdp = md_buf;
+                npairs++;
             }
             if (new_len >= start_len) {
 #ifdef LZG_PROF
@@ -1248,24 +1264,25 @@ struct Enc {
                 uint32_t normal_match_price = match_price + dm0(E_IS_REP + st);
                 extend_to(len_end, cur + new_len, cur);
                 uint32_t offs = 0;
-                while (offs + 1 < npairs && start_len > md_len[offs]) offs++;
+                while (offs + 1 < npairs && start_len > md_l(offs)) offs++;
                 uint32_t seg_lo = start_len;
                 for (uint32_t seg_guard = 0;; seg_guard++) {
 #ifdef LZG_PROF
                     if (seg_guard) tm = PCLK();
 #endif
-                    if (seg_guard > (uint32_t)kMdCap || md_len[offs] < seg_lo) { bad = 6; break; }
-                    uint32_t seg_hi = md_len[offs];
-                    uint32_t cur_back = md_dist[offs];
+                    if (seg_guard > (uint32_t)kMdCap || md_l(offs) < seg_lo) { bad = 6; break; }
+                    uint32_t seg_hi = md_l(offs);
+                    uint32_t cur_back = md_d(offs);
                     relax_match(cur, seg_lo, seg_hi, normal_match_price, cur_back, pos_state, cur);
                     PEND(PF_RELAX, tm);
                     uint32_t lt = seg_hi;
-                    if (lt < num_avail_full) {
+                    const int side = offs < 2 ? 5 + (int)offs : -1;
+                    const uint64_t gmp = offs == 0 ? gmp0 : gmp1;
+                    if (lt < num_avail_full && (side < 0 || lt + 3 >= 64u || ((gmp >> (lt + 2)) & 3u) == 3u)) {
                         uint32_t t = num_avail_full - 1 - lt;
                         if (t > fb) t = fb;
                         PBEGIN(tm2);
-                        const int side = offs < 2 ? 5 + (int)offs : -1;
-                        uint32_t lt2 = side > 0 ? glen(offs == 0 ? gmp0 : gmp1, cur_back, (int32_t)lt + 1, (int32_t)t)
+                        uint32_t lt2 = side > 0 ? glen(gmp, cur_back, (int32_t)lt + 1, (int32_t)t)
                                                 : match_len((int32_t)lt, cur_back, (int32_t)t);
                         PEND(PF_TWOLEN, tm2);
                         if (lt2 >= 2) {
@@ -1349,7 +1366,7 @@ struct Enc {
             }
             prev_byte = cb;   // the match's last byte
         }
-        q_run(q);
+        q_run(q, back == -1 && !eos_marker);
         if (len_coder >= 0) {   // LenPriceTableEncoder.Encode (LenPriceTableEncoder.java:31-37)
             const uint32_t c = lenc[len_coder * 16 + ps] - 1;
             lenc[len_coder * 16 + ps] = c;
@@ -1448,14 +1465,14 @@ struct Enc {
 
 // LDS layout of one stream's workgroup; shared by the kernel (carving) and
 // the host (dynamic LDS size). Regions are 16-byte aligned.
-enum { L_PP, L_PROBS, L_DMP, L_LENP, L_LENC, L_PSP, L_DP, L_AP, L_TP, L_MDLEN, L_MDDIST, L_RINFO, L_RPAIRS, L_OPRICE,
+enum { L_PP, L_PROBS, L_DMP, L_LENP, L_LENC, L_PSP, L_DP, L_AP, L_TP, L_MDBUF, L_RINFO, L_RPAIRS, L_OPRICE,
        L_OPP, L_OBP, L_OBP2, L_OFS, L_OBACKS, L_OBYTES, L_WIN, L_RBUF, L_LIT, L_COUNT };
 __host__ __device__ inline uint32_t enc_lds_layout(const EncArgs& a, uint32_t* off) {
     const uint32_t md_cap = a.fb + 2;   // pairs per position <= fb (+1 clamp slot)
     const uint32_t sz[L_COUNT] = {
         512 * 2, prob_count(a.pb) * 2 + 2, dm_count(a.pb) * 4 + 4, 2 * (1u << a.pb) * a.len_table_size * 2, 2 * 16 * 4, 256 * 2, 512 * 2, 16 * 4,
-        0u /* tp aliases the gather window */, md_cap * 2, md_cap * 4, kRing * 4, kRing * kInlinePairs * a.pair_bytes,
-        (kOptLds + 2) * 4, (kOptLds + 2) * 4, (kOptLds + 2) * 4, (kOptLds + 2) * 4, kOptLds + 2, 4 * kOptLds * 4, kOptLds * 4, kSides * kGW, kRbuf * 2 + 2,
+        0u /* tp aliases the gather window */, md_cap * a.pair_bytes, kRing * 4, kRing * kInlinePairs * a.pair_bytes,
+        (kOptLds + 2) * 4, (kOptLds + 2) * 4, (kOptLds + 2) * 4, (kOptLds + 2) * 4, kOptLds + 2, 4 * kOptLds * 4, kOptLds * 4, kWinBytes, kRbuf * 2 + 2,
         a.lit_in_lds ? (0x300u << (a.lc + a.lp)) * 2 + 2 : 0u};
     uint32_t o = 0;
     for (int i = 0; i < L_COUNT; i++) { if (off) off[i] = o; o += (sz[i] + 15) & ~15u; }
@@ -1492,8 +1509,8 @@ __global__ void __launch_bounds__(kWave, 4) enc_kernel(EncArgs a) {
     e.ap = (uint32_t*)(smem + off[L_AP]);
     e.tp = (uint16_t*)(smem + off[L_WIN]);   // tempPrices only live inside fill_distances_prices
     e.dmp = (uint32_t*)(smem + off[L_DMP]);
-    e.md_len = (uint16_t*)(smem + off[L_MDLEN]);
-    e.md_dist = (uint32_t*)(smem + off[L_MDDIST]);
+    e.md_buf = (PairT*)(smem + off[L_MDBUF]);
+    e.mdp = e.md_buf;
     e.ring_info = (uint32_t*)(smem + off[L_RINFO]);
     e.ring_pairs = (PairT*)(smem + off[L_RPAIRS]);
     e.o_price = (uint32_t*)(smem + off[L_OPRICE]);

@@ -137,7 +137,9 @@ __global__ void __launch_bounds__(64) mf_prev2_kernel(const uint64_t* __restrict
 }
 
 // exclusive prefix sum of v over the block's threads; wsum: (blockDim / 64) words of LDS.
-// One block barrier; the caller synchronises before wsum is written again.
+// One block barrier; the caller synchronises before wsum is written again (or passes
+// another wsum): a wave that leaves the barrier early must not overwrite words the
+// slower waves are still reading.
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* wsum) {
     const uint32_t tid = threadIdx.x, lane = tid % 64, w = tid / 64;
     uint32_t x = v;
@@ -187,8 +189,9 @@ __global__ void __launch_bounds__(kChainThreads) mf_chains_kernel(const uint64_t
                                                                    uint64_t* __restrict__ seg_end, uint32_t long_min,
                                                                    uint32_t* __restrict__ cls, uint32_t* __restrict__ long_raw) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];   // dynamic LDS (the CPU emulation shares it)
-    uint32_t* wsum = (uint32_t*)smem;                                   // [kChainThreads / 64]
-    uint32_t* tile_tot = wsum + kChainThreads / 64;                     // [2]: heads, valid items
+    uint32_t* wsum = (uint32_t*)smem;                                   // [kChainThreads / 64]: the head-count scan
+    uint32_t* wsum2 = wsum + kChainThreads / 64;                        // [kChainThreads / 64]: the valid-item scan
+    uint32_t* tile_tot = wsum2 + kChainThreads / 64;                    // [2]: heads, valid items
     const uint32_t tid = threadIdx.x, s = blockIdx.x;
     const uint64_t lo = offs[s], n = offs[s + 1] - lo;
     uint32_t run = 0, valid = 0;
@@ -212,7 +215,10 @@ __global__ void __launch_bounds__(kChainThreads) mf_chains_kernel(const uint64_t
         for (uint32_t j = 0; j < kChainItems; j++)
             if (head & (1u << j)) chain_start[lo + c++] = (uint32_t)(lo + b0 + j);
         if (tid == kChainThreads - 1) tile_tot[0] = ex + cnt;
-        const uint32_t vex = block_excl_scan(nv, wsum + 0);   // barrier inside: tile_tot[0] is visible after it
+        // a scan of its own words: with the same words, a wave through the first scan's barrier
+        // overwrote them while slower waves still summed them (wrong chain starts; seen only when
+        // other kernels share the CU and skew the waves: the encode-beside-decode fault of round 3)
+        const uint32_t vex = block_excl_scan(nv, wsum2);   // barrier inside: tile_tot[0] is visible after it
         if (tid == kChainThreads - 1) tile_tot[1] = vex + nv;
         __syncthreads();
         run += tile_tot[0];
@@ -646,7 +652,7 @@ int run_match_finder(Ctx* ctx, const Derived& d, const uint8_t* in, const uint64
     {
         TimedLaunch tl(ctx, "mf_sort", st);
         hipMemsetAsync(w.cls, 0, 96 * sizeof(uint32_t), st);
-        hipLaunchKernelGGL(mf_chains_kernel, dim3(nstreams), dim3(kChainThreads), (kChainThreads / 64 + 2) * 4, st, d_offs, w.ks,
+        hipLaunchKernelGGL(mf_chains_kernel, dim3(nstreams), dim3(kChainThreads), (2 * (kChainThreads / 64) + 2) * 4, st, d_offs, w.ks,
                            w.chain_start, w.chain_len, okey, w.chain_idx, w.seg_end, long_min, w.cls, long_raw);
         hipLaunchKernelGGL(mf_chain_scan_kernel, dim3(1), dim3(kChainThreads), (kChainThreads / 64 + 2) * 4, st, d_offs, w.seg_end,
                            nstreams, w.chain_offs);

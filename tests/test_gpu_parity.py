@@ -424,7 +424,8 @@ def test_gpu_config4_shape_one_stream_longer_than_dict(ctx, heartbeat):
     dictionary (72 MiB at dict 2^26, L5), so the window expires for the last 8 MiB
     (matchMinPos, BinTree.java:164, 231) and the pairs are the 64-bit form (> 8 MiB).
     Encoder.Code (Encoder.java:1064-1077) on the whole stream: byte-equal to the oracle.
-    The parse is one wave's serial chain (the solo kernel), ~0.45 MB/s: minutes."""
+    The parse is one wave's serial chain (the batch parse kernel with one stream), ~0.45 MB/s:
+    minutes."""
     n = 72 << 20
     data = lzma_amd.bench_generate(n)
     p = lzma_amd.make_params(dict_size=1 << 26, fb=32, mf=1, lc=3, lp=0, pb=2)

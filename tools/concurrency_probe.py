@@ -83,6 +83,19 @@ def main():
     res["dec_concurrent_ms"] = done.get("dec_ms")
     res["dec_ok"] = done.get("dec_ok", False) and bool(torch.equal(d_dec, d_in))
     res["enc_ok"] = bool(np.array_equal(lens, lens2))
+    if res["enc_ok"]:   # every stream of the concurrent encode byte-equal to the sequential one
+        d_pack2 = torch.empty_like(d_pack)
+        pk2 = ctx.pack_dev(d_comp2, cap_offs, lens2, d_pack2, sa.cuda_stream)
+        torch.cuda.synchronize()
+        res["enc_bytes_equal"] = bool(np.array_equal(pk, pk2)) and bool(torch.equal(d_pack[:int(pk[-1])], d_pack2[:int(pk2[-1])]))
+        # and a sample of them equal to the oracle's Encoder.Code bytes
+        sys.path.insert(0, os.path.join(REPO, "tests"))
+        import oracle_ffi as orc
+        idx = np.linspace(0, n - 1, 16).astype(int)
+        hp = d_pack2[:int(pk2[-1])].cpu().numpy()
+        ref = orc.encode_many([host[int(offs[i]):int(offs[i + 1])].tobytes() for i in idx],
+                              orc.params(1 << 26, 32, 1, 3, 0, 2, 0), threads=orc.cpu_threads())
+        res["oracle_sample_equal"] = all(hp[int(pk2[i]):int(pk2[i + 1])].tobytes() == r for i, r in zip(idx, ref))
     res["timings"] = {k: round(v[0], 1) for k, v in ctx.timings().items()}
     print(json.dumps(res), flush=True)
 
