@@ -42,16 +42,17 @@ constexpr int kOptLds = 64;         // _optimum slots kept in LDS (deeper slots 
 constexpr uint32_t kOptMask = kOptLds - 1;   // RING: slot i lives in entry i & kOptMask
 constexpr uint32_t kFarEntry = kOptLds + 1;   // RING: the entry of slot cur + 65 until cur + 1 retires
 static_assert((kOptLds & (kOptLds - 1)) == 0, "the _optimum ring is a power of two");
-constexpr int kLitLdsMaxBits = 1;   // literal coders in LDS when lc + lp <= 1 (<= 3 KiB); else HBM/L2
+constexpr int kLitLdsMaxBits = 1;   // literal coders in LDS when lc + lp <= 1 (<= 3 KiB); else HBM/L2 ...
+constexpr int kLitLdsMaxBitsFew = 3;   // ... or lc + lp <= 3 (12 KiB) when a launch has few streams per CU
+constexpr int kFewStreams = 1024;      // "few": up to 4 streams per CU (LDS for 16 streams per CU is spoken for)
 constexpr int kMdCap = kMatchMaxLen + 1;
 constexpr int kRing = 32;           // match-info prefetch window (positions)
 constexpr int kGW = 64;             // gather window: offsets -1 .. kGW-2 around the current position
 constexpr int kGI = kGW / kWave;    // gather iterations per side (1 on hardware)
-constexpr int kSides = 7;           // gathered sides: cur, rep0..rep3, pair0, pair1 (only cur's bytes go to LDS)
-constexpr int kWinBytes = 2 * kNumFullDistances;   // LDS: the cur side's kGW bytes, aliased by tempPrices
+constexpr int kSides = 7;           // gathered sides: cur, rep0..rep3, pair0, pair1 (masks only, no bytes in LDS)
+constexpr int kTpBytes = 2 * kNumFullDistances;   // tempPrices (u16 [kNumFullDistances])
 constexpr int kRbuf = 128;          // coder-record staging ring (records, power of two; halves of 64 go to HBM)
 constexpr int kLitSlots = (8 + kWave - 1) / kWave;   // literal bits per lane (1 on hardware)
-static_assert(kWinBytes >= kGW, "the gather window holds the cur side");
 
 #define FI __device__ __forceinline__
 // Lanes of one wavefront exchange data through LDS. The hardware runs one
@@ -87,6 +88,17 @@ static_assert(kWinBytes >= kGW, "the gather window holds the cur side");
 #define PEND(k, v) do {} while (0)
 #define PCOUNT(k) do {} while (0)
 #endif
+
+// A ballot over this wave's lanes. The CPU emulation (LZG_WAVE = 1) runs each wave as
+// one lane: its own bit, with no collective across the block (the two-wave kernel's
+// waves run different code, and the emulation's collectives are block-wide).
+FI uint64_t wballot(bool p) {
+#if LZG_WAVE == 1
+    return p ? 1ull : 0ull;
+#else
+    return __ballot(p);
+#endif
+}
 
 FI uint64_t uni64(uint64_t v) {
     return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32)) << 32) |
@@ -124,8 +136,30 @@ FI uint32_t sel4(uint32_t i, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
 // FairPrio rows of the encoder's waves (lzma_common.h)
 __device__ uint32_t g_enc_sched[kSchedRows * kSchedCols];
 
-template <typename PairT, bool LIT_LDS, int PBS, bool RING>
+// The two-wave parse (W2, few streams per CU): wave 0 (A) runs the serial chain, wave 1
+// (B) the candidate relaxations of a forward position (R) beside A's state / gather /
+// literal-price work for the next one (S). Each round is two workgroup barriers: P (B has
+// finished R(c); A has finished S(c + 1)) and Q (A has updated slot c + 1's literal /
+// short-rep candidates and handed R(c + 1) over). Everything B needs crosses in this LDS
+// record, which A writes only between P and Q (B reads it right after Q); slot contents
+// are shared through the _optimum ring itself.
+enum : uint32_t { kPipeIdle = 0, kPipeRelax = 1, kPipeExit = 2 };
+struct Pipe {
+    uint32_t ctrl;
+    uint32_t cur, position, st, pos_state, cur_and1, cur_byte, match_byte;
+    uint32_t next_is_char, match_price, rep_match_price, new_len, npairs;
+    uint32_t gp, mfpos, md_off, mdbuf_off;
+    uint32_t rp0, rp1, rp2, rp3;
+    uint32_t len_end, ring_top, far_valid, bad;   // the pass's shared state: B's during R, A's otherwise
+    uint32_t pad;
+    uint64_t gm0, gm1, gm2, gm3, gmp0, gmp1;
+};
+
+template <typename PairT, bool LIT_LDS, int PBS, bool RING, bool W2 = false>
 struct Enc {
+    // W2: a 64-entry match-list ring filled 32 entries at a time (A's fill for c + 1 keeps
+    // c's entry, which B still reads), and md_buf double-buffered
+    static constexpr uint32_t kRingN = W2 ? 2 * (uint32_t)kRing : (uint32_t)kRing;
     using PP = PairPack<PairT>;
     using PL = ProbLayout<PBS>;
     static constexpr int E_IS_MATCH = PL::IS_MATCH, E_IS_REP = PL::IS_REP, E_G0 = PL::G0, E_G1 = PL::G1,
@@ -147,6 +181,9 @@ struct Enc {
     uint16_t* tp;             // tempPrices [128]
     const PairT* mdp;         // the current position's pairs (packed): its ring slot, or md_buf
     PairT* md_buf;            // a copy when the list is longer than the inline pairs or is clamped
+    PairT* md_buf_alt;        // W2: the other position's md_buf
+    uint8_t* lds_base;        // W2: LDS offsets in the hand-off
+    Pipe* pipe;               // W2: the hand-off record
     uint32_t* ring_info;      // [kRing]
     PairT* ring_pairs;        // [kRing * kInlinePairs]
     uint32_t* o_price;        // _optimum SoA, [kOptLds] each (+ the sink entry, + kFarEntry)
@@ -157,7 +194,6 @@ struct Enc {
     uint32_t* o_backs;        // [4][kOptLds]
     uint32_t* o_bytes;        // [kOptLds] cur byte | match byte << 8 | previous byte << 16 of each parsed
                               // position, so the coder needs no HBM byte loads (RING: | state << 24)
-    uint8_t* win;             // gather window: the cur side's bytes at offsets -1 .. kGW - 2
     uint16_t* rbuf;           // coder-record staging ring [kRbuf]
     __amdgpu_buffer_rsrc_t spill;   // _optimum slots >= kOptLds in HBM (9 fields x kNumOpts dwords)
     // ---- parameters
@@ -265,7 +301,6 @@ struct Enc {
         const uint32_t r = i & kOptMask;
         LANE_FOR(uint32_t, k, 0u, 5u) sstore(5 + k, i, k < 4 ? o_backs[k * kOptLds + r] : o_bytes[r]);
     }
-    // the gather window's bytes of the current position (see gather())
     // pair k of the current position's match list
     FI uint32_t md_l(uint32_t k) const { return PP::len(mdp[k]); }
     FI uint32_t md_d(uint32_t k) const { return PP::dist(mdp[k]); }
@@ -358,7 +393,7 @@ struct Enc {
         for (int32_t i0 = 0; i0 < limit; i0 += kWave) {
             int32_t i = i0 + (int32_t)lane;
             bool ne = i < limit ? (in_byte(a + (uint32_t)i) != in_byte(b + (uint32_t)i)) : true;
-            uint64_t m = __ballot(ne);
+            uint64_t m = wballot(ne);
             if (m) {
                 int32_t r = i0 + (__ffsll((long long)m) - 1);
                 return (uint32_t)(r < limit ? r : limit);
@@ -373,9 +408,9 @@ struct Enc {
     // o = -1 .. kGW-2 from p (the current byte) on the cur side and at
     // p + o - dist - 1 on the rep / match sides. gather() issues all of those
     // byte loads at once (one lane per offset, one memory round trip), keeps
-    // equality masks per side (bit o+1 = bytes equal at offset o) and stores
-    // the bytes in the LDS window for the literal-price lookups. Compares past
-    // the window fall back to match_len.
+    // equality masks per side (bit o+1 = bytes equal at offset o) and keeps the
+    // three bytes the position step prices its literal with in scalars. Compares
+    // past the window fall back to match_len.
     FI void gather(bool with_pairs) {
         gp = mfpos - 1;
         const uint32_t d0 = rp0 + 1, d1 = rp1 + 1, d2 = rp2 + 1, d3 = rp3 + 1;
@@ -393,15 +428,13 @@ struct Enc {
         for (int it = 0; it < kGI; it++) {
             const int sh = it * kWave;
             const uint32_t k = (uint32_t)sh + lane;
-            gm0 |= (uint64_t)__ballot(va[it] == v0[it]) << sh;
-            gm1 |= (uint64_t)__ballot(va[it] == v1[it]) << sh;
-            gm2 |= (uint64_t)__ballot(va[it] == v2[it]) << sh;
-            gm3 |= (uint64_t)__ballot(va[it] == v3[it]) << sh;
-            win[k] = (uint8_t)va[it];   // the cur side only: the other sides' bytes are read (rarely, by a
-                                         // two-step candidate's literal) straight from the stream
+            gm0 |= (uint64_t)wballot(va[it] == v0[it]) << sh;
+            gm1 |= (uint64_t)wballot(va[it] == v1[it]) << sh;
+            gm2 |= (uint64_t)wballot(va[it] == v2[it]) << sh;
+            gm3 |= (uint64_t)wballot(va[it] == v3[it]) << sh;
             if (with_pairs) {
-                gmp0 |= (uint64_t)__ballot(va[it] == w0[it]) << sh;
-                gmp1 |= (uint64_t)__ballot(va[it] == w1[it]) << sh;
+                gmp0 |= (uint64_t)wballot(va[it] == w0[it]) << sh;
+                gmp1 |= (uint64_t)wballot(va[it] == w1[it]) << sh;
             }
         }
         // the three bytes every position step reads, straight from the loaded registers
@@ -412,9 +445,9 @@ struct Enc {
         LANE_FENCE();
     }
     // byte at p + o on the cur side
-    FI uint32_t a_byte(int32_t o) const {
-        return (o >= -1 && o <= kGW - 2) ? (uint32_t)win[o + 1] : in_byte(gp + (uint32_t)o);
-    }
+    // only a two-step candidate's literal (a few percent of the positions) reads one: from the
+    // stream (the gather keeps no bytes in LDS)
+    FI uint32_t a_byte(int32_t o) const { return in_byte(gp + (uint32_t)o); }
     // byte at p + o - dist - 1 (side 1..6 = rep0..3, pair0..1; side < 0: not gathered); only a
     // two-step candidate's literal reads one (a few percent of the positions): from the stream
     FI uint32_t b_byte(int side, uint32_t dist, int32_t o) const {
@@ -652,6 +685,7 @@ struct Enc {
     FI void ring_fill(uint32_t base) {
         ring_base = base;
         LANE_FOR(uint32_t, k, 0u, (uint32_t)kRing) {
+            const uint32_t e = W2 ? ((base + k) & (kRingN - 1)) : k;   // the ring entry of position base + k
             uint32_t q = base + k;
             uint32_t info = 0;
             PairT p0 = 0, p1 = 0, p2 = 0, p3 = 0;
@@ -662,8 +696,8 @@ struct Enc {
                 info = load_rec<PairT>(pairs + g0 * rec_vecs<PairT>(), q);
                 p0 = q[0]; p1 = q[1]; p2 = q[2]; p3 = q[3];
             }
-            ring_info[k] = info;
-            PairT* dst = ring_pairs + k * kInlinePairs;
+            ring_info[e] = info;
+            PairT* dst = ring_pairs + e * kInlinePairs;
             dst[0] = p0; dst[1] = p1; dst[2] = p2; dst[3] = p3;
         }
         LANE_FENCE();
@@ -672,7 +706,8 @@ struct Enc {
         PBEGIN(t0);
         uint32_t q = mfpos;
         if (q - ring_base >= (uint32_t)kRing) ring_fill(q);
-        uint32_t slot = q - ring_base;
+        const uint32_t slot = W2 ? (q & (kRingN - 1)) : q - ring_base;
+        if (W2) { PairT* t = md_buf; md_buf = md_buf_alt; md_buf_alt = t; }   // B may still hold the last list
         uint32_t info = ring_info[slot];
         uint32_t cnt = info & 0xFFFFu, ml = info >> 16;
         if (cnt <= (uint32_t)kInlinePairs) {   // read in place from the ring: no copy, no LDS round trip
@@ -1046,6 +1081,7 @@ struct Enc {
             else relax_first<false>(lstart, len_main, npairs, normal_match_price, pos_state);
         }
         PEND(PF_RELAX, t2);
+        if (W2) return parse_forward_w2(position, back_res, len_end);
         return parse_forward(position, back_res, len_end);
     }
 
@@ -1054,14 +1090,23 @@ struct Enc {
     // of cur + 1. F: every slot touched (<= cur + 1) is below kOptLds, so the
     // slot accesses are plain LDS operations (no spill branches, and no wait on
     // outstanding HBM operations merged into them).
-    template <bool F>
-    FI bool pos_step(uint32_t cur, uint32_t position, uint32_t& st, uint32_t& pos_state, uint32_t& cur_and1,
-                     uint32_t& match_price, uint32_t& rep_match_price, uint32_t& cur_byte, uint32_t& match_byte) {
+    // It is two parts: S (pos_state_part: the state, the reps, the gather and the literal
+    // price of cur; reads slot cur and its predecessors, all final) and N (pos_next_part:
+    // the literal / short-rep update of slot cur + 1, which cur - 1's longer candidates may
+    // have written). The two-wave kernel (W2) runs S of cur + 1 beside R of cur.
+    struct PosS { uint32_t st, pos_state, cur_price, cur_and1, cur_byte, match_byte; };
+    // COMMIT = false (W2): the slot writes wait for pos_commit, after the exit checks -- a
+    // speculative S of the pass's last slot must not overwrite the ring entry whose
+    // behind fields (slot cur - 64) the coder may still read
+    template <bool F, bool COMMIT = true>
+    FI PosS pos_state_part(uint32_t cur, uint32_t position) {
         PBEGIN(ts);
         // F: cur + 1 < kOptLds, every slot touched is in LDS. RING deep steps: the
         // ahead fields of cur and cur + 1 are in the ring (FA); the behind fields of
         // pprev may be in HBM (a path back by 65), checked per access.
         constexpr bool FA = F || RING, FB = F;
+        PosS r;
+        uint32_t st;
         uint32_t ppc = pp_at<FA>(cur);
         uint32_t pos_prev_c = ppc & 0xFFFFu;
         uint32_t fsc = fs_at<FA>(cur);
@@ -1101,48 +1146,220 @@ struct Enc {
                 rp0 = (uint32_t)(pos - kNumRepDistances); rp1 = b0; rp2 = b1; rp3 = b2;
             }
         }
-        if (RING) {   // cur's entry held cur - 64
-            if (!F && cur >= (uint32_t)kOptLds) evict_behind(cur - (uint32_t)kOptLds);
-        } else set_fs<FA>(cur, (fsc & 0xFu) | (st << 4));
-        set_back<FA>(cur, 0, rp0); set_back<FA>(cur, 1, rp1); set_back<FA>(cur, 2, rp2); set_back<FA>(cur, 3, rp3);
-        uint32_t cur_price = price_at<FA>(cur);
-        pos_state = position & ps_mask;
-        // cur + 1's slot: nothing before its literal / short-rep update below writes it, so its
-        // reads are issued before the gather and complete under the gather's memory round trip
-        uint32_t nx = cur + 1;
-        uint32_t nx_price = price_at<FA>(nx);
-        uint32_t nx_pp = pp_at<FA>(nx);
-        int32_t nx_bp = bp_at<FA>(nx);
+        if (COMMIT) {
+            if (RING) {   // cur's entry held cur - 64
+                if (!F && cur >= (uint32_t)kOptLds) evict_behind(cur - (uint32_t)kOptLds);
+            } else set_fs<FA>(cur, (fsc & 0xFu) | (st << 4));
+            set_back<FA>(cur, 0, rp0); set_back<FA>(cur, 1, rp1); set_back<FA>(cur, 2, rp2); set_back<FA>(cur, 3, rp3);
+        }
+        r.cur_price = price_at<FA>(cur);
+        r.pos_state = position & ps_mask;
+        r.st = st;
         PEND(PF_STATE, ts);
+        return r;
+    }
+    template <bool F, bool COMMIT = true>
+    FI void pos_gather_part(uint32_t cur, uint32_t position, PosS& r) {
+        constexpr bool FA = F || RING;
         PBEGIN(tg);
         gather(true);
-        set_bytes<FA>(cur, win_bytes() | (RING ? st << 24 : 0u));
+        if (COMMIT) set_bytes<FA>(cur, win_bytes() | (RING ? r.st << 24 : 0u));
         PEND(PF_REPLEN, tg);
-        cur_byte = g_cur;
-        match_byte = g_mb;
+        r.cur_byte = g_cur;
+        r.match_byte = g_mb;
         PBEGIN(tl);
-        cur_and1 = cur_price + dm0(E_IS_MATCH + (st << PBS) + pos_state) +
-                            lit_price(lit_coder(position, g_prev), !st_is_char(st), match_byte, cur_byte);
+        r.cur_and1 = r.cur_price + dm0(E_IS_MATCH + (r.st << PBS) + r.pos_state) +
+                     lit_price(lit_coder(position, g_prev), !st_is_char(r.st), r.match_byte, r.cur_byte);
         PEND(PF_LIT, tl);
+    }
+    // W2 (RING only): the slot writes S deferred, once the step is known to run
+    template <bool F>
+    FI void pos_commit(uint32_t cur, const PosS& r) {
+        if (!F && cur >= (uint32_t)kOptLds) evict_behind(cur - (uint32_t)kOptLds);
+        set_back<true>(cur, 0, rp0); set_back<true>(cur, 1, rp1); set_back<true>(cur, 2, rp2); set_back<true>(cur, 3, rp3);
+        set_bytes<true>(cur, win_bytes() | (r.st << 24));
+    }
+    // N: slot cur + 1's literal and short-rep candidates (nx_*: its fields, read by the caller)
+    template <bool F>
+    FI bool pos_next_part(uint32_t cur, const PosS& r, uint32_t nx_price, uint32_t nx_pp, int32_t nx_bp, uint32_t nx_fs,
+                          uint32_t& match_price, uint32_t& rep_match_price) {
+        constexpr bool FA = F || RING;
         PBEGIN(tn);
+        const uint32_t nx = cur + 1, st = r.st, pos_state = r.pos_state;
         bool next_is_char = false;
-        if (cur_and1 < nx_price) {
-            nx_price = cur_and1; nx_pp = (nx_pp & 0xFFFF0000u) | cur; nx_bp = -1;
-            set_price<FA>(nx, nx_price); set_pp<FA>(nx, nx_pp); set_bp<FA>(nx, -1); set_fs<FA>(nx, fs_at<FA>(nx) & ~1u);
+        if (r.cur_and1 < nx_price) {
+            nx_price = r.cur_and1; nx_pp = (nx_pp & 0xFFFF0000u) | cur; nx_bp = -1;
+            set_price<FA>(nx, nx_price); set_pp<FA>(nx, nx_pp); set_bp<FA>(nx, -1); set_fs<FA>(nx, nx_fs & ~1u);
             next_is_char = true;
         }
-        match_price = cur_price + dm1(E_IS_MATCH + (st << PBS) + pos_state);
+        match_price = r.cur_price + dm1(E_IS_MATCH + (st << PBS) + pos_state);
         rep_match_price = match_price + dm1(E_IS_REP + st);
-        if (match_byte == cur_byte && !((nx_pp & 0xFFFFu) < cur && nx_bp == 0)) {
+        if (r.match_byte == r.cur_byte && !((nx_pp & 0xFFFFu) < cur && nx_bp == 0)) {
             uint32_t srp = rep_match_price + rep_len1_price(st, pos_state);
             if (srp <= nx_price) {
-                set_price<FA>(nx, srp); set_pp<FA>(nx, (nx_pp & 0xFFFF0000u) | cur); set_bp<FA>(nx, 0); set_fs<FA>(nx, fs_at<FA>(nx) & ~1u);
+                set_price<FA>(nx, srp); set_pp<FA>(nx, (nx_pp & 0xFFFF0000u) | cur); set_bp<FA>(nx, 0); set_fs<FA>(nx, nx_fs & ~1u);
                 next_is_char = true;
             }
         }
         fence_upto(nx);
         PEND(PF_STATE, tn);
         return next_is_char;
+    }
+    template <bool F>
+    FI bool pos_step(uint32_t cur, uint32_t position, PosS& r, uint32_t& match_price, uint32_t& rep_match_price) {
+        constexpr bool FA = F || RING;
+        r = pos_state_part<F>(cur, position);
+        // cur + 1's slot: nothing before its literal / short-rep update below writes it, so its
+        // reads are issued before the gather and complete under the gather's memory round trip
+        const uint32_t nx = cur + 1;
+        const uint32_t nx_price = price_at<FA>(nx), nx_pp = pp_at<FA>(nx), nx_fs = fs_at<FA>(nx);
+        const int32_t nx_bp = bp_at<FA>(nx);
+        pos_gather_part<F>(cur, position, r);
+        return pos_next_part<F>(cur, r, nx_price, nx_pp, nx_bp, nx_fs, match_price, rep_match_price);
+    }
+
+    // R: the rest of position cur's step (Encoder.java:743-808): the literal + rep0
+    // look-ahead, the rep candidates and the match candidates with their two-step
+    // look-aheads, relaxing slots >= cur + 2 (len_end grows with them).
+    FI void relax_step(uint32_t cur, uint32_t position, const PosS& r, bool next_is_char, uint32_t match_price,
+                       uint32_t rep_match_price, uint32_t new_len, uint32_t npairs, uint32_t& len_end) {
+        const uint32_t st = r.st, pos_state = r.pos_state, cur_and1 = r.cur_and1;
+        const uint32_t match_byte = r.match_byte, cur_byte = r.cur_byte;
+        if (RING && far_valid) {   // slot cur + 64 leaves the far entry for cur's, free now
+            evict_ahead(cur);
+            const uint32_t rr = cur & kOptMask, e = kFarEntry;
+            const uint32_t fp = o_price[e], fpp = o_pp[e], ffs = o_fs[e];
+            const int32_t fbp = o_bp[e], fbp2 = o_bp2[e];
+            o_price[rr] = fp; o_pp[rr] = fpp; o_bp[rr] = fbp; o_bp2[rr] = fbp2; o_fs[rr] = (uint8_t)ffs;
+            ring_top = cur + (uint32_t)kOptLds;
+            far_valid = 0;
+            LANE_FENCE();
+        }
+        uint32_t num_avail_full = avail() + 1;
+        if ((uint32_t)kNumOpts - 1 - cur < num_avail_full) num_avail_full = kNumOpts - 1 - cur;
+        uint32_t num_avail = num_avail_full;
+        if (num_avail < 2) return;
+        if (num_avail > fb) num_avail = fb;
+        // literal + rep0: lenTest2 >= 2 needs the bytes at offsets 1 and 2 equal (mask bits 2, 3)
+        if (!next_is_char && match_byte != cur_byte && (gm0 & 0xCu) == 0xCu) {
+            uint32_t t = num_avail_full - 1 < fb ? num_avail_full - 1 : fb;
+            PBEGIN(t2a);
+            uint32_t lt2 = glen(gm0, rp0, 1, (int32_t)t);
+            PEND(PF_TWOLEN, t2a);
+            if (lt2 >= 2) {
+                PBEGIN(t2b);
+                uint32_t st2 = st_lit(st);
+                uint32_t psn = (position + 1) & ps_mask;
+                uint32_t nrmp = cur_and1 + dm1(E_IS_MATCH + (st2 << PBS) + psn) + dm1(E_IS_REP + st2);
+                uint32_t offset = cur + 1 + lt2;
+                extend_to(len_end, offset, cur);
+                relax_two_step(offset, nrmp + rep_price(0, lt2, st2, psn), cur + 1, false, 0, 0, cur);
+                PEND(PF_RELAX, t2b);
+            }
+        }
+        uint32_t start_len = 2;
+#pragma unroll
+        for (uint32_t ri = 0; ri < (uint32_t)kNumRepDistances; ri++) {
+            uint32_t rdist = sel4(ri, rp0, rp1, rp2, rp3);
+            const uint64_t gmr = ri == 0 ? gm0 : (ri == 1 ? gm1 : (ri == 2 ? gm2 : gm3));
+            // lenTest >= 2 needs offsets 0 and 1 equal (mask bits 1, 2): most reps stop here
+            if ((gmr & 6u) != 6u) continue;
+            PBEGIN(tr);
+            uint32_t lt = glen(gmr, rdist, 0, (int32_t)num_avail);
+            PEND(PF_REPLEN, tr);
+            if (lt < 2) continue;
+            PBEGIN(trr);
+            extend_to(len_end, cur + lt, cur);
+            relax_rep(cur, 2, lt, rep_match_price + pure_rep_price(ri, st, pos_state), pos_state, cur, ri);
+            PEND(PF_RELAX, trr);
+            if (ri == 0) start_len = lt + 1;
+            // the two-step lenTest2 >= 2 needs offsets lt + 1 and lt + 2 equal (mask bits lt + 2, lt + 3)
+            if (lt < num_avail_full && (lt + 3 >= 64u || ((gmr >> (lt + 2)) & 3u) == 3u)) {
+                uint32_t t = num_avail_full - 1 - lt;
+                if (t > fb) t = fb;
+                PBEGIN(tq);
+                uint32_t lt2 = glen(gmr, rdist, (int32_t)lt + 1, (int32_t)t);
+                PEND(PF_TWOLEN, tq);
+                if (lt2 >= 2) {
+                    PBEGIN(tq2);
+                    uint32_t st2 = st_long(st);
+                    uint32_t psn = (position + lt) & ps_mask;
+                    uint32_t clcp = rep_match_price + rep_price(ri, lt, st, pos_state) +
+                                    dm0(E_IS_MATCH + (st2 << PBS) + psn) +
+                                    lit_price(lit_coder(position + lt, a_byte((int32_t)lt - 1)), true,
+                                              b_byte(1 + (int)ri, rdist, (int32_t)lt), a_byte((int32_t)lt));
+                    st2 = st_lit(st2);
+                    psn = (position + lt + 1) & ps_mask;
+                    uint32_t nrmp = clcp + dm1(E_IS_MATCH + (st2 << PBS) + psn) + dm1(E_IS_REP + st2);
+                    uint32_t offset = lt + 1 + lt2;
+                    extend_to(len_end, cur + offset, cur);
+                    relax_two_step(cur + offset, nrmp + rep_price(0, lt2, st2, psn), cur + lt + 1, true, cur, (int32_t)ri, cur);
+                    PEND(PF_TWOREL, tq2);
+                }
+            }
+        }
+        if (new_len > num_avail) {
+            new_len = num_avail;
+            uint32_t np0 = npairs;
+            for (npairs = 0; npairs + 1 < np0 && new_len > md_l(npairs); npairs++) {}
+            // the clamped list goes to md_buf (the ring slot stays the match finder's)
+            LANE_FOR(uint32_t, k, 0u, npairs + 1)
+                md_buf[k] = k < npairs ? mdp[k] : PP::pack(new_len, md_d(npairs));
+            LANE_FENCE();
+            mdp = md_buf;
+            npairs++;
+        }
+        if (new_len >= start_len) {
+#ifdef LZG_PROF
+            uint64_t tm = PCLK();
+#endif
+            uint32_t normal_match_price = match_price + dm0(E_IS_REP + st);
+            extend_to(len_end, cur + new_len, cur);
+            uint32_t offs = 0;
+            while (offs + 1 < npairs && start_len > md_l(offs)) offs++;
+            uint32_t seg_lo = start_len;
+            for (uint32_t seg_guard = 0;; seg_guard++) {
+#ifdef LZG_PROF
+                if (seg_guard) tm = PCLK();
+#endif
+                if (seg_guard > (uint32_t)kMdCap || md_l(offs) < seg_lo) { bad = 6; break; }
+                uint32_t seg_hi = md_l(offs);
+                uint32_t cur_back = md_d(offs);
+                relax_match(cur, seg_lo, seg_hi, normal_match_price, cur_back, pos_state, cur);
+                PEND(PF_RELAX, tm);
+                uint32_t lt = seg_hi;
+                const int side = offs < 2 ? 5 + (int)offs : -1;
+                const uint64_t gmp = offs == 0 ? gmp0 : gmp1;
+                if (lt < num_avail_full && (side < 0 || lt + 3 >= 64u || ((gmp >> (lt + 2)) & 3u) == 3u)) {
+                    uint32_t t = num_avail_full - 1 - lt;
+                    if (t > fb) t = fb;
+                    PBEGIN(tm2);
+                    uint32_t lt2 = side > 0 ? glen(gmp, cur_back, (int32_t)lt + 1, (int32_t)t)
+                                            : match_len((int32_t)lt, cur_back, (int32_t)t);
+                    PEND(PF_TWOLEN, tm2);
+                    if (lt2 >= 2) {
+                        PBEGIN(tm3);
+                        uint32_t cl = normal_match_price + pos_len_price(cur_back, lt, pos_state);
+                        uint32_t st2 = st_match(st);
+                        uint32_t psn = (position + lt) & ps_mask;
+                        uint32_t clcp = cl + dm0(E_IS_MATCH + (st2 << PBS) + psn) +
+                                        lit_price(lit_coder(position + lt, a_byte((int32_t)lt - 1)), true,
+                                                  b_byte(side, cur_back, (int32_t)lt), a_byte((int32_t)lt));
+                        st2 = st_lit(st2);
+                        psn = (position + lt + 1) & ps_mask;
+                        uint32_t nrmp = clcp + dm1(E_IS_MATCH + (st2 << PBS) + psn) + dm1(E_IS_REP + st2);
+                        uint32_t offset = lt + 1 + lt2;
+                        extend_to(len_end, cur + offset, cur);
+                        relax_two_step(cur + offset, nrmp + rep_price(0, lt2, st2, psn), cur + lt + 1, true, cur,
+                                       (int32_t)(cur_back + kNumRepDistances), cur);
+                        PEND(PF_TWOREL, tm3);
+                    }
+                }
+                offs++;
+                if (offs == npairs) break;
+                seg_lo = seg_hi + 1;
+            }
+        }
     }
 
     FI uint32_t parse_forward(uint32_t position, int32_t* back_res, uint32_t len_end) {
@@ -1164,152 +1381,141 @@ struct Enc {
                 return backward(back_res, cur);
             }
             position++;
-            uint32_t st, pos_state, cur_and1, match_price, rep_match_price, cur_byte, match_byte;
+            PosS r;
+            uint32_t match_price, rep_match_price;
             // every slot the step touches is <= cur + 1: LDS only when that is below kOptLds
 #ifdef LZG_PROF
             if (cur + 1 >= (uint32_t)kOptLds) PCOUNT(PF_NSPILL);
 #endif
-            const bool next_is_char =
-                cur + 1 < (uint32_t)kOptLds
-                    ? pos_step<true>(cur, position, st, pos_state, cur_and1, match_price, rep_match_price, cur_byte, match_byte)
-                    : pos_step<false>(cur, position, st, pos_state, cur_and1, match_price, rep_match_price, cur_byte, match_byte);
-            if (RING && far_valid) {   // slot cur + 64 leaves the far entry for cur's, free now
-                evict_ahead(cur);
-                const uint32_t r = cur & kOptMask, e = kFarEntry;
-                const uint32_t fp = o_price[e], fpp = o_pp[e], ffs = o_fs[e];
-                const int32_t fbp = o_bp[e], fbp2 = o_bp2[e];
-                o_price[r] = fp; o_pp[r] = fpp; o_bp[r] = fbp; o_bp2[r] = fbp2; o_fs[r] = (uint8_t)ffs;
-                ring_top = cur + (uint32_t)kOptLds;
-                far_valid = 0;
-                LANE_FENCE();
-            }
-            uint32_t num_avail_full = avail() + 1;
-            if ((uint32_t)kNumOpts - 1 - cur < num_avail_full) num_avail_full = kNumOpts - 1 - cur;
-            uint32_t num_avail = num_avail_full;
-            if (num_avail < 2) continue;
-            if (num_avail > fb) num_avail = fb;
-            // literal + rep0: lenTest2 >= 2 needs the bytes at offsets 1 and 2 equal (mask bits 2, 3)
-            if (!next_is_char && match_byte != cur_byte && (gm0 & 0xCu) == 0xCu) {
-                uint32_t t = num_avail_full - 1 < fb ? num_avail_full - 1 : fb;
-                PBEGIN(t2a);
-                uint32_t lt2 = glen(gm0, rp0, 1, (int32_t)t);
-                PEND(PF_TWOLEN, t2a);
-                if (lt2 >= 2) {
-                    PBEGIN(t2b);
-                    uint32_t st2 = st_lit(st);
-                    uint32_t psn = (position + 1) & ps_mask;
-                    uint32_t nrmp = cur_and1 + dm1(E_IS_MATCH + (st2 << PBS) + psn) + dm1(E_IS_REP + st2);
-                    uint32_t offset = cur + 1 + lt2;
-                    extend_to(len_end, offset, cur);
-                    relax_two_step(offset, nrmp + rep_price(0, lt2, st2, psn), cur + 1, false, 0, 0, cur);
-                    PEND(PF_RELAX, t2b);
-                }
-            }
-            uint32_t start_len = 2;
-#pragma unroll
-            for (uint32_t ri = 0; ri < (uint32_t)kNumRepDistances; ri++) {
-                uint32_t rdist = sel4(ri, rp0, rp1, rp2, rp3);
-                const uint64_t gmr = ri == 0 ? gm0 : (ri == 1 ? gm1 : (ri == 2 ? gm2 : gm3));
-                // lenTest >= 2 needs offsets 0 and 1 equal (mask bits 1, 2): most reps stop here
-                if ((gmr & 6u) != 6u) continue;
-                PBEGIN(tr);
-                uint32_t lt = glen(gmr, rdist, 0, (int32_t)num_avail);
-                PEND(PF_REPLEN, tr);
-                if (lt < 2) continue;
-                PBEGIN(trr);
-                extend_to(len_end, cur + lt, cur);
-                relax_rep(cur, 2, lt, rep_match_price + pure_rep_price(ri, st, pos_state), pos_state, cur, ri);
-                PEND(PF_RELAX, trr);
-                if (ri == 0) start_len = lt + 1;
-                // the two-step lenTest2 >= 2 needs offsets lt + 1 and lt + 2 equal (mask bits lt + 2, lt + 3)
-                if (lt < num_avail_full && (lt + 3 >= 64u || ((gmr >> (lt + 2)) & 3u) == 3u)) {
-                    uint32_t t = num_avail_full - 1 - lt;
-                    if (t > fb) t = fb;
-                    PBEGIN(tq);
-                    uint32_t lt2 = glen(gmr, rdist, (int32_t)lt + 1, (int32_t)t);
-                    PEND(PF_TWOLEN, tq);
-                    if (lt2 >= 2) {
-                        PBEGIN(tq2);
-                        uint32_t st2 = st_long(st);
-                        uint32_t psn = (position + lt) & ps_mask;
-                        uint32_t clcp = rep_match_price + rep_price(ri, lt, st, pos_state) +
-                                        dm0(E_IS_MATCH + (st2 << PBS) + psn) +
-                                        lit_price(lit_coder(position + lt, a_byte((int32_t)lt - 1)), true,
-                                                  b_byte(1 + (int)ri, rdist, (int32_t)lt), a_byte((int32_t)lt));
-                        st2 = st_lit(st2);
-                        psn = (position + lt + 1) & ps_mask;
-                        uint32_t nrmp = clcp + dm1(E_IS_MATCH + (st2 << PBS) + psn) + dm1(E_IS_REP + st2);
-                        uint32_t offset = lt + 1 + lt2;
-                        extend_to(len_end, cur + offset, cur);
-                        relax_two_step(cur + offset, nrmp + rep_price(0, lt2, st2, psn), cur + lt + 1, true, cur, (int32_t)ri, cur);
-                        PEND(PF_TWOREL, tq2);
-                    }
-                }
-            }
-            if (new_len > num_avail) {
-                new_len = num_avail;
-                uint32_t np0 = npairs;
-                for (npairs = 0; npairs + 1 < np0 && new_len > md_l(npairs); npairs++) {}
-                // the clamped list goes to md_buf (the ring slot stays the match finder's)
-                LANE_FOR(uint32_t, k, 0u, npairs + 1)
-                    md_buf[k] = k < npairs ? mdp[k] : PP::pack(new_len, md_d(npairs));
-                LANE_FENCE();
-                mdp = md_buf;
-                npairs++;
-            }
-            if (new_len >= start_len) {
-#ifdef LZG_PROF
-                uint64_t tm = PCLK();
-#endif
-                uint32_t normal_match_price = match_price + dm0(E_IS_REP + st);
-                extend_to(len_end, cur + new_len, cur);
-                uint32_t offs = 0;
-                while (offs + 1 < npairs && start_len > md_l(offs)) offs++;
-                uint32_t seg_lo = start_len;
-                for (uint32_t seg_guard = 0;; seg_guard++) {
-#ifdef LZG_PROF
-                    if (seg_guard) tm = PCLK();
-#endif
-                    if (seg_guard > (uint32_t)kMdCap || md_l(offs) < seg_lo) { bad = 6; break; }
-                    uint32_t seg_hi = md_l(offs);
-                    uint32_t cur_back = md_d(offs);
-                    relax_match(cur, seg_lo, seg_hi, normal_match_price, cur_back, pos_state, cur);
-                    PEND(PF_RELAX, tm);
-                    uint32_t lt = seg_hi;
-                    const int side = offs < 2 ? 5 + (int)offs : -1;
-                    const uint64_t gmp = offs == 0 ? gmp0 : gmp1;
-                    if (lt < num_avail_full && (side < 0 || lt + 3 >= 64u || ((gmp >> (lt + 2)) & 3u) == 3u)) {
-                        uint32_t t = num_avail_full - 1 - lt;
-                        if (t > fb) t = fb;
-                        PBEGIN(tm2);
-                        uint32_t lt2 = side > 0 ? glen(gmp, cur_back, (int32_t)lt + 1, (int32_t)t)
-                                                : match_len((int32_t)lt, cur_back, (int32_t)t);
-                        PEND(PF_TWOLEN, tm2);
-                        if (lt2 >= 2) {
-                            PBEGIN(tm3);
-                            uint32_t cl = normal_match_price + pos_len_price(cur_back, lt, pos_state);
-                            uint32_t st2 = st_match(st);
-                            uint32_t psn = (position + lt) & ps_mask;
-                            uint32_t clcp = cl + dm0(E_IS_MATCH + (st2 << PBS) + psn) +
-                                            lit_price(lit_coder(position + lt, a_byte((int32_t)lt - 1)), true,
-                                                      b_byte(side, cur_back, (int32_t)lt), a_byte((int32_t)lt));
-                            st2 = st_lit(st2);
-                            psn = (position + lt + 1) & ps_mask;
-                            uint32_t nrmp = clcp + dm1(E_IS_MATCH + (st2 << PBS) + psn) + dm1(E_IS_REP + st2);
-                            uint32_t offset = lt + 1 + lt2;
-                            extend_to(len_end, cur + offset, cur);
-                            relax_two_step(cur + offset, nrmp + rep_price(0, lt2, st2, psn), cur + lt + 1, true, cur,
-                                           (int32_t)(cur_back + kNumRepDistances), cur);
-                            PEND(PF_TWOREL, tm3);
-                        }
-                    }
-                    offs++;
-                    if (offs == npairs) break;
-                    seg_lo = seg_hi + 1;
-                }
-            }
+            const bool next_is_char = cur + 1 < (uint32_t)kOptLds ? pos_step<true>(cur, position, r, match_price, rep_match_price)
+                                                                   : pos_step<false>(cur, position, r, match_price, rep_match_price);
+            relax_step(cur, position, r, next_is_char, match_price, rep_match_price, new_len, npairs, len_end);
         }
         __builtin_unreachable();   // the loop returns
+    }
+
+    // ------------------------------------------------------------ two-wave parse (W2)
+    FI void pipe_sync() { __syncthreads(); }   // one workgroup barrier (both waves)
+    // A: hand R(cur) to B (ctrl kPipeRelax), or stop B (kPipeIdle / kPipeExit)
+    FI void publish(uint32_t ctrl, uint32_t cur, uint32_t position, const PosS& r, bool next_is_char, uint32_t match_price,
+                    uint32_t rep_match_price, uint32_t new_len, uint32_t npairs, uint32_t len_end) {
+        Pipe* P = pipe;
+        P->ctrl = ctrl;
+        P->len_end = len_end; P->ring_top = ring_top; P->far_valid = far_valid; P->bad = bad;
+        if (ctrl == kPipeRelax) {
+            P->cur = cur; P->position = position; P->st = r.st; P->pos_state = r.pos_state; P->cur_and1 = r.cur_and1;
+            P->cur_byte = r.cur_byte; P->match_byte = r.match_byte;
+            P->next_is_char = next_is_char ? 1u : 0u; P->match_price = match_price; P->rep_match_price = rep_match_price;
+            P->new_len = new_len; P->npairs = npairs;
+            P->gp = gp; P->mfpos = mfpos;
+            P->md_off = (uint32_t)((const uint8_t*)mdp - lds_base); P->mdbuf_off = (uint32_t)((uint8_t*)md_buf - lds_base);
+            P->rp0 = rp0; P->rp1 = rp1; P->rp2 = rp2; P->rp3 = rp3;
+            P->gm0 = gm0; P->gm1 = gm1; P->gm2 = gm2; P->gm3 = gm3; P->gmp0 = gmp0; P->gmp1 = gmp1;
+        }
+        LANE_FENCE();
+    }
+    // A: the forward loop of getOptimum with R on wave B (same slot updates, same order:
+    // R(c) ends before N(c + 1) starts, and S(c + 1) reads only slots R(c) never writes)
+    FI uint32_t parse_forward_w2(uint32_t position, int32_t* back_res, uint32_t len_end) {
+        uint32_t cur = 1;
+        if (++wd > wd_max) bad = 103;
+        if (bad) { *back_res = -1; return 1; }
+        if (cur == len_end) return backward(back_res, cur);
+        if (len_end >= (uint32_t)kNumOpts) { bad = 4; *back_res = -1; return 1; }
+        uint32_t new_len = read_match_distances();
+        if (new_len >= fb) {
+            longest_len = new_len;
+            longest_found = 1;
+            return backward(back_res, cur);
+        }
+        position++;
+        PosS r;
+        uint32_t match_price, rep_match_price;
+        bool next_is_char = pos_step<true>(cur, position, r, match_price, rep_match_price);   // cur + 1 = 2 < kOptLds
+        // A writes the record only between P and Q: B reads it right after Q, and by the next
+        // P it is done with it (here: B's read of the last pass's kPipeIdle)
+        pipe_sync();   // P
+        publish(kPipeRelax, cur, position, r, next_is_char, match_price, rep_match_price, new_len, num_pairs, len_end);
+        pipe_sync();   // Q: B runs R(cur)
+        for (;;) {
+            // S(cur + 1), speculative: the exit checks need R(cur)'s len_end
+            const uint32_t nc = cur + 1;
+            const uint32_t sv_mfpos = mfpos;
+            const int32_t sv_addoff = additional_offset;
+            const bool spec = nc < (uint32_t)kNumOpts - 1;
+            uint32_t nnew = 0;
+            PosS nr{};
+            if (spec) {
+                nnew = read_match_distances();
+                if (nnew < fb) {
+                    if (nc + 1 < (uint32_t)kOptLds) { nr = pos_state_part<true, false>(nc, position + 1); pos_gather_part<true, false>(nc, position + 1, nr); }
+                    else { nr = pos_state_part<false, false>(nc, position + 1); pos_gather_part<false, false>(nc, position + 1, nr); }
+                }
+            }
+            pipe_sync();   // P: R(cur) is done
+            {
+                const Pipe* P = pipe;
+                len_end = P->len_end; ring_top = P->ring_top; far_valid = P->far_valid;
+                if (P->bad && !bad) bad = P->bad;
+            }
+            cur = nc;
+            if (++wd > wd_max && !bad) bad = 103;
+            int32_t ret_back = -1;
+            uint32_t ret = 0;   // 0: the step runs; else the value getOptimum returns
+            if (bad) ret = 1;
+            else if (cur == len_end) {   // the pass ends before this position's read: undo it
+                if (spec) { mfpos = sv_mfpos; additional_offset = sv_addoff; }
+                ret = 2;
+            } else if (cur >= (uint32_t)kNumOpts - 1 || len_end >= (uint32_t)kNumOpts) { bad = 4; ret = 1; }
+            else if (nnew >= fb) { longest_len = nnew; longest_found = 1; ret = 2; }
+            if (ret) {
+                publish(kPipeIdle, 0, 0, r, false, 0, 0, 0, 0, len_end);
+                pipe_sync();   // Q: B goes back to wait
+                if (ret == 2) return backward(back_res, cur);
+                *back_res = ret_back;
+                return 1;
+            }
+            position++;
+            new_len = nnew;
+            // N(cur): slot cur + 1, now that R(cur - 1) is done
+            const uint32_t nx = cur + 1;
+            const uint32_t nx_price = price_at<true>(nx), nx_pp = pp_at<true>(nx), nx_fs = fs_at<true>(nx);
+            const int32_t nx_bp = bp_at<true>(nx);
+            if (nx < (uint32_t)kOptLds) { pos_commit<true>(cur, nr); next_is_char = pos_next_part<true>(cur, nr, nx_price, nx_pp, nx_bp, nx_fs, match_price, rep_match_price); }
+            else { pos_commit<false>(cur, nr); next_is_char = pos_next_part<false>(cur, nr, nx_price, nx_pp, nx_bp, nx_fs, match_price, rep_match_price); }
+            r = nr;
+            publish(kPipeRelax, cur, position, r, next_is_char, match_price, rep_match_price, new_len, num_pairs, len_end);
+            pipe_sync();   // Q: B runs R(cur)
+        }
+    }
+    // B: waits for R steps until A stops it
+    FI void relax_wave() {
+        for (;;) {
+            pipe_sync();   // P
+            pipe_sync();   // Q
+            const Pipe* P = pipe;
+            const uint32_t ctrl = P->ctrl;
+            if (ctrl == kPipeExit) return;
+            if (ctrl != kPipeRelax) continue;
+            PosS r;
+            const uint32_t cur = P->cur, position = P->position;
+            r.st = P->st; r.pos_state = P->pos_state; r.cur_and1 = P->cur_and1; r.cur_byte = P->cur_byte;
+            r.match_byte = P->match_byte; r.cur_price = 0;
+            const bool next_is_char = P->next_is_char != 0;
+            const uint32_t match_price = P->match_price, rep_match_price = P->rep_match_price;
+            const uint32_t new_len = P->new_len, npairs = P->npairs;
+            gp = P->gp; mfpos = P->mfpos;
+            mdp = (const PairT*)(lds_base + P->md_off);
+            md_buf = (PairT*)(lds_base + P->mdbuf_off);
+            rp0 = P->rp0; rp1 = P->rp1; rp2 = P->rp2; rp3 = P->rp3;
+            gm0 = P->gm0; gm1 = P->gm1; gm2 = P->gm2; gm3 = P->gm3; gmp0 = P->gmp0; gmp1 = P->gmp1;
+            uint32_t len_end = P->len_end;
+            ring_top = P->ring_top; far_valid = P->far_valid; bad = 0;
+            relax_step(cur, position, r, next_is_char, match_price, rep_match_price, new_len, npairs, len_end);
+            Pipe* W = pipe;
+            W->len_end = len_end; W->ring_top = ring_top; W->far_valid = far_valid; W->bad = bad;
+            LANE_FENCE();
+        }
     }
 
     // ------------------------------------------------------------ emitters (Encoder.java:860-1024, 818-841)
@@ -1466,14 +1672,16 @@ struct Enc {
 // LDS layout of one stream's workgroup; shared by the kernel (carving) and
 // the host (dynamic LDS size). Regions are 16-byte aligned.
 enum { L_PP, L_PROBS, L_DMP, L_LENP, L_LENC, L_PSP, L_DP, L_AP, L_TP, L_MDBUF, L_RINFO, L_RPAIRS, L_OPRICE,
-       L_OPP, L_OBP, L_OBP2, L_OFS, L_OBACKS, L_OBYTES, L_WIN, L_RBUF, L_LIT, L_COUNT };
+       L_OPP, L_OBP, L_OBP2, L_OFS, L_OBACKS, L_OBYTES, L_TPBUF, L_RBUF, L_LIT, L_PIPE, L_MDBUF2, L_COUNT };
 __host__ __device__ inline uint32_t enc_lds_layout(const EncArgs& a, uint32_t* off) {
     const uint32_t md_cap = a.fb + 2;   // pairs per position <= fb (+1 clamp slot)
     const uint32_t sz[L_COUNT] = {
         512 * 2, prob_count(a.pb) * 2 + 2, dm_count(a.pb) * 4 + 4, 2 * (1u << a.pb) * a.len_table_size * 2, 2 * 16 * 4, 256 * 2, 512 * 2, 16 * 4,
-        0u /* tp aliases the gather window */, md_cap * a.pair_bytes, kRing * 4, kRing * kInlinePairs * a.pair_bytes,
-        (kOptLds + 2) * 4, (kOptLds + 2) * 4, (kOptLds + 2) * 4, (kOptLds + 2) * 4, kOptLds + 2, 4 * kOptLds * 4, kOptLds * 4, kWinBytes, kRbuf * 2 + 2,
-        a.lit_in_lds ? (0x300u << (a.lc + a.lp)) * 2 + 2 : 0u};
+        0u /* L_TP: unused (tempPrices are L_TPBUF) */, md_cap * a.pair_bytes, (a.w2 ? 2u : 1u) * kRing * 4,
+        (a.w2 ? 2u : 1u) * kRing * kInlinePairs * a.pair_bytes,
+        (kOptLds + 2) * 4, (kOptLds + 2) * 4, (kOptLds + 2) * 4, (kOptLds + 2) * 4, kOptLds + 2, 4 * kOptLds * 4, kOptLds * 4, kTpBytes, kRbuf * 2 + 2,
+        a.lit_in_lds ? (0x300u << (a.lc + a.lp)) * 2 + 2 : 0u,
+        a.w2 ? (uint32_t)sizeof(Pipe) : 0u, a.w2 ? md_cap * a.pair_bytes : 0u};
     uint32_t o = 0;
     for (int i = 0; i < L_COUNT; i++) { if (off) off[i] = o; o += (sz[i] + 15) & ~15u; }
     return o;
@@ -1482,11 +1690,16 @@ __host__ __device__ inline uint32_t enc_lds_layout(const EncArgs& a, uint32_t* o
 // SPEC = 1: the level-5 parameters of bench.py (fb 32, lc 3, lp 0, pb 2, no end
 // marker) as compile-time constants; SPEC = 2: any parameters with fb <= 32;
 // SPEC = 0: fb > 32. SPEC 1 and 2 keep _optimum in the LDS ring.
-template <typename PairT, bool LIT_LDS, int PBS, int SPEC>
-__global__ void __launch_bounds__(kWave, 4) enc_kernel(EncArgs a) {
+// W2 (SPEC 1 and 2 only): two waves per stream (Enc::parse_forward_w2 / relax_wave), for
+// launches with few streams per CU; their register budget is 256 per lane (2 waves per SIMD).
+template <typename PairT, bool LIT_LDS, int PBS, int SPEC, bool W2 = false>
+__global__ void __launch_bounds__(W2 ? 2 * kWave : kWave, W2 ? 2 : 4) enc_kernel(EncArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    Enc<PairT, LIT_LDS, PBS, (SPEC != 0)> e;   // SPEC 1 and 2: fb <= 32, the _optimum ring
-    e.lane = threadIdx.x;
+    static_assert(!W2 || SPEC != 0, "the two-wave parse needs the _optimum ring (fb <= 32)");
+    Enc<PairT, LIT_LDS, PBS, (SPEC != 0), W2> e;   // SPEC 1 and 2: fb <= 32, the _optimum ring
+    // the wave index is wave-uniform: readfirstlane makes that visible (scalar branches on it)
+    const uint32_t wave = W2 ? (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave)) : 0u;
+    e.lane = threadIdx.x % kWave;
     if (SPEC == 1) {
         e.fb = 32; e.lc = 3; e.lp = 0; e.pb = 2; e.ps_mask = 3; e.eos = 0; e.tsize = 31;
     } else {
@@ -1497,7 +1710,8 @@ __global__ void __launch_bounds__(kWave, 4) enc_kernel(EncArgs a) {
     uint32_t off[L_COUNT];
     {
         EncArgs la = a;   // SPEC: the layout folds to constants (immediate LDS offsets, no SGPR per region)
-        if (SPEC == 1) { la.fb = 32; la.pb = 2; la.lc = 3; la.lp = 0; la.lit_in_lds = 0; la.pair_bytes = 4; la.len_table_size = 31; }
+        if (SPEC == 1) { la.fb = 32; la.pb = 2; la.lc = 3; la.lp = 0; la.lit_in_lds = LIT_LDS ? 1 : 0; la.pair_bytes = 4; la.len_table_size = 31; }
+        la.w2 = W2 ? 1u : 0u;
         enc_lds_layout(la, off);
     }
     e.pp = (uint16_t*)(smem + off[L_PP]);
@@ -1507,7 +1721,7 @@ __global__ void __launch_bounds__(kWave, 4) enc_kernel(EncArgs a) {
     e.psp = (uint16_t*)(smem + off[L_PSP]);
     e.dp = (uint16_t*)(smem + off[L_DP]);
     e.ap = (uint32_t*)(smem + off[L_AP]);
-    e.tp = (uint16_t*)(smem + off[L_WIN]);   // tempPrices only live inside fill_distances_prices
+    e.tp = (uint16_t*)(smem + off[L_TPBUF]);   // tempPrices (FillDistancesPrices' scratch)
     e.dmp = (uint32_t*)(smem + off[L_DMP]);
     e.md_buf = (PairT*)(smem + off[L_MDBUF]);
     e.mdp = e.md_buf;
@@ -1520,14 +1734,19 @@ __global__ void __launch_bounds__(kWave, 4) enc_kernel(EncArgs a) {
     e.o_fs = smem + off[L_OFS];
     e.o_backs = (uint32_t*)(smem + off[L_OBACKS]);
     e.o_bytes = (uint32_t*)(smem + off[L_OBYTES]);
-    e.win = smem + off[L_WIN];
     e.rbuf = (uint16_t*)(smem + off[L_RBUF]);
+    if (W2) {
+        e.lds_base = smem;
+        e.pipe = (Pipe*)(smem + off[L_PIPE]);
+        e.md_buf_alt = (PairT*)(smem + off[L_MDBUF2]);
+    }
     uint8_t* scratch = a.scratch + (size_t)blockIdx.x * a.scratch_stride;
     e.spill = __builtin_amdgcn_make_buffer_rsrc(scratch, 0, kNumOpts * 4 * 10, 0x00020000);
     uint16_t* lit_g = (uint16_t*)(a.lit_scratch + (size_t)blockIdx.x * a.lit_stride);
     if (LIT_LDS) e.lit = (uint16_t*)(smem + off[L_LIT]);
     else e.lit = lit_g;
-    for (int i0 = 0; i0 < 512; i0 += kWave) e.pp[i0 + e.lane] = (uint16_t)c_tab.prices[i0 + e.lane];
+    if (wave == 0)
+        for (int i0 = 0; i0 < 512; i0 += kWave) e.pp[i0 + e.lane] = (uint16_t)c_tab.prices[i0 + e.lane];
     LANE_FENCE();
     e.dbg = a.dbg;
 #ifdef LZG_DEBUG
@@ -1544,7 +1763,7 @@ __global__ void __launch_bounds__(kWave, 4) enc_kernel(EncArgs a) {
     const int s = __builtin_amdgcn_readfirstlane((int)a.order[blockIdx.x]);
     if (s < 0 || s >= a.nstreams) return;   // a corrupt order entry: touch nothing (the host checked the order it wrote)
     if (uni64(a.offs[s + 1]) < uni64(a.offs[s]) || uni64(a.rec_offs[s + 1]) < uni64(a.rec_offs[s])) {
-        if (e.lane == 0) { a.rec_lens[s] = 0; a.out_lens[s] = 9ull << 32; a.status[s] = LZMA_E_INTERNAL; }
+        if (wave == 0 && e.lane == 0) { a.rec_lens[s] = 0; a.out_lens[s] = 9ull << 32; a.status[s] = LZMA_E_INTERNAL; }
         return;
     }
     e.gbase = uni64(a.offs[s]);
@@ -1557,12 +1776,22 @@ __global__ void __launch_bounds__(kWave, 4) enc_kernel(EncArgs a) {
 #ifdef LZG_DEBUG
     if (e.dbg && e.lane == 0) __hip_atomic_store(e.dbg + 8, (uint32_t)s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 #endif
+    if (W2 && wave == 1) {   // B: relax steps until A's exit
+        e.relax_wave();
+        return;
+    }
 #ifdef LZG_PROF
     const uint64_t t_run = __builtin_amdgcn_s_memtime();
     const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
 #endif
     e.run();
     e.prio.finish(e.lane);
+    if (W2) {   // B waits at a barrier pair for its next step: release it
+        typename Enc<PairT, LIT_LDS, PBS, (SPEC != 0), W2>::PosS r0{};
+        e.pipe_sync();   // P
+        e.publish(kPipeExit, 0, 0, r0, false, 0, 0, 0, 0, 0);
+        e.pipe_sync();   // Q
+    }
 #ifdef LZG_PROF
     e.prof[PF_TOTAL] = __builtin_amdgcn_s_memtime() - t_run;
     e.prof[PF_T0] = rt0;   // 100 MHz wall clock: where each stream ran
@@ -1586,21 +1815,35 @@ size_t enc_scratch_per_block(const Derived&) { return (size_t)kNumOpts * 4 * 10 
 
 size_t enc_lit_bytes(const Derived& d) { return ((size_t)0x300 << (d.lc + d.lp)) * 2 + 2; }   // + the sink entry
 
-uint32_t enc_lit_in_lds(const Derived& d) { return (d.lc + d.lp) <= (uint32_t)kLitLdsMaxBits; }
+uint32_t enc_lit_in_lds(const Derived& d, int nstreams) {
+    static const int force = getenv("LZG_ENC_LITLDS") ? atoi(getenv("LZG_ENC_LITLDS")) : -1;   // A/B runs
+    const uint32_t bits = d.lc + d.lp;
+    if (bits <= (uint32_t)kLitLdsMaxBits) return 1;
+    if (force >= 0) return force != 0 && bits <= (uint32_t)kLitLdsMaxBitsFew;
+    return nstreams <= kFewStreams && bits <= (uint32_t)kLitLdsMaxBitsFew;
+}
 
 int enc_grid(const Derived&, int nstreams) { return nstreams; }   // one workgroup per stream
 
 template <typename PairT, bool LIT, int PBS, int SPEC>
 static void launch_spec(Ctx* ctx, const EncArgs& a, int grid, size_t lds, hipStream_t st) {
+    TimedLaunch tl(ctx, "enc_parse", st);
+    if constexpr (SPEC != 0) {
+        if (a.w2) {
+            if (lds > 64 * 1024)
+                hipFuncSetAttribute((const void*)enc_kernel<PairT, LIT, PBS, SPEC, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            hipLaunchKernelGGL((enc_kernel<PairT, LIT, PBS, SPEC, true>), dim3(grid), dim3(2 * kWave), lds, st, a);
+            return;
+        }
+    }
     if (lds > 64 * 1024)
         hipFuncSetAttribute((const void*)enc_kernel<PairT, LIT, PBS, SPEC>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    TimedLaunch tl(ctx, "enc_parse", st);
     hipLaunchKernelGGL((enc_kernel<PairT, LIT, PBS, SPEC>), dim3(grid), dim3(kWave), lds, st, a);
 }
 
 template <typename PairT, bool LIT, int PBS>
 static void launch_one(Ctx* ctx, const EncArgs& a, int grid, size_t lds, hipStream_t st) {
-    if constexpr (std::is_same<PairT, uint32_t>::value && !LIT && PBS == 2) {
+    if constexpr (std::is_same<PairT, uint32_t>::value && PBS == 2) {
         if (a.fb == 32 && a.lc == 3 && a.lp == 0 && a.pb == 2 && a.eos == 0) {
             launch_spec<PairT, LIT, PBS, 1>(ctx, a, grid, lds, st);
             return;
@@ -1616,8 +1859,21 @@ static void launch_pb(Ctx* ctx, const EncArgs& a, int grid, size_t lds, hipStrea
     else launch_one<PairT, LIT, 4>(ctx, a, grid, lds, st);
 }
 
-int launch_encoder(Ctx* ctx, const EncArgs& a, bool wide_pairs, int grid, hipStream_t st) {
-    if (a.pair_bytes != (wide_pairs ? 8u : 4u)) return ctx->fail(LZMA_E_INTERNAL, "pair width mismatch");
+// The two-wave parse for launches with few streams per CU (a single long stream, strong
+// scaling's share of a buffer; up to 4 per CU: 2 waves per SIMD at 256 VGPRs). Measured on
+// MI355X it runs as fast as the one-wave parse and no faster (DESIGN.md section 5, round 4:
+// R is the small part of a position; S and N, the chain, stay serial), so it is off unless
+// LZG_ENC_W2=1 (the CPU emulation test runs both forms).
+static bool want_w2(const EncArgs& a, int grid) {
+    if (a.fb > 32) return false;   // the ring (SPEC 1 / 2) only
+    static const int force = getenv("LZG_ENC_W2") ? atoi(getenv("LZG_ENC_W2")) : -1;
+    return force > 0 && grid <= kFewStreams;
+}
+
+int launch_encoder(Ctx* ctx, const EncArgs& a0, bool wide_pairs, int grid, hipStream_t st) {
+    if (a0.pair_bytes != (wide_pairs ? 8u : 4u)) return ctx->fail(LZMA_E_INTERNAL, "pair width mismatch");
+    EncArgs a = a0;
+    a.w2 = want_w2(a, grid) ? 1u : 0u;
     size_t lds = enc_lds_bytes(a);
     if (lds > 160 * 1024) return ctx->fail(LZMA_E_PARAM, "encoder LDS %zu too large", lds);
     if (wide_pairs) {

@@ -314,6 +314,7 @@ struct EncArgs {
     uint32_t fb, lc, lp, pb, eos, dist_table_size, len_table_size;
     uint32_t lit_in_lds;
     uint32_t pair_bytes;          // 4 (u32 packed pairs) or 8 (u64, streams >= 8 MiB)
+    uint32_t w2;                  // two waves per stream (enc.hip W2: few streams per CU); set by launch_encoder
     uint32_t* dbg;                // debug checkpoints (host-mapped, LZMA_MI355X_DEBUG only) or null
     uint64_t* prof;               // phase cycles [nstreams][kProfSlots] (LZG_PROF builds) or null
 };
@@ -343,7 +344,7 @@ int launch_rc(Ctx* ctx, const RcArgs& a, hipStream_t st);
 // records one stream of n bytes can need: <= 21 per byte (a length-2 match: isMatch, isRep,
 // 4 length bits, 6 slot bits, 30 footer bits), the end marker (42) and the first literal
 __host__ __device__ inline uint64_t rc_record_bound(uint64_t n) { return (24 * n + 64 + 63) & ~(uint64_t)63; }
-uint32_t enc_lit_in_lds(const Derived& d);
+uint32_t enc_lit_in_lds(const Derived& d, int nstreams);
 size_t enc_scratch_per_block(const Derived& d);
 size_t enc_lit_bytes(const Derived& d);
 

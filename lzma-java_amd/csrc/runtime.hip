@@ -265,7 +265,7 @@ static int encode_pass(Ctx* ctx, const Derived& d, const uint8_t* d_in, const ui
         a.lit_scratch = ctx->litbuf;
         a.fb = d.fb; a.lc = d.lc; a.lp = d.lp; a.pb = d.pb; a.eos = d.eos;
         a.dist_table_size = d.dist_table_size; a.len_table_size = d.len_table_size;
-        a.lit_in_lds = enc_lit_in_lds(d);
+        a.lit_in_lds = enc_lit_in_lds(d, grid);
         a.pair_bytes = wide ? 8 : 4;
         LZG_TRACE(ctx, st, "encode pass: %d streams, %llu bytes, grid %d", ns, (unsigned long long)total, grid);
         DebugWatch watch;
