@@ -49,8 +49,9 @@ constexpr int kMdCap = kMatchMaxLen + 1;
 constexpr int kRing = 32;           // match-info prefetch window (positions)
 constexpr int kGW = 64;             // gather window: offsets -1 .. kGW-2 around the current position
 constexpr int kGI = kGW / kWave;    // gather iterations per side (1 on hardware)
-constexpr int kSides = 7;           // gathered sides: cur, rep0..rep3, pair0, pair1 (masks only, no bytes in LDS)
-constexpr int kTpBytes = 2 * kNumFullDistances;   // tempPrices (u16 [kNumFullDistances])
+constexpr int kSides = 7;           // gathered sides: cur, rep0..rep3, pair0, pair1 (only cur's bytes go to LDS)
+constexpr int kTpBytes = 2 * kNumFullDistances;   // tempPrices (u16 [kNumFullDistances]); the cur side's window aliases it
+static_assert(kTpBytes >= kGW, "the gather window holds the cur side");
 constexpr int kRbuf = 128;          // coder-record staging ring (records, power of two; halves of 64 go to HBM)
 constexpr int kLitSlots = (8 + kWave - 1) / kWave;   // literal bits per lane (1 on hardware)
 
@@ -148,7 +149,7 @@ struct Pipe {
     uint32_t ctrl;
     uint32_t cur, position, st, pos_state, cur_and1, cur_byte, match_byte;
     uint32_t next_is_char, match_price, rep_match_price, new_len, npairs;
-    uint32_t gp, mfpos, md_off, mdbuf_off;
+    uint32_t gp, mfpos, md_off, mdbuf_off, win_off;
     uint32_t rp0, rp1, rp2, rp3;
     uint32_t len_end, ring_top, far_valid, bad;   // the pass's shared state: B's during R, A's otherwise
     uint32_t pad;
@@ -158,7 +159,7 @@ struct Pipe {
 template <typename PairT, bool LIT_LDS, int PBS, bool RING, bool W2 = false>
 struct Enc {
     // W2: a 64-entry match-list ring filled 32 entries at a time (A's fill for c + 1 keeps
-    // c's entry, which B still reads), and md_buf double-buffered
+    // c's entry, which B still reads), and md_buf / the gather window double-buffered
     static constexpr uint32_t kRingN = W2 ? 2 * (uint32_t)kRing : (uint32_t)kRing;
     using PP = PairPack<PairT>;
     using PL = ProbLayout<PBS>;
@@ -182,6 +183,8 @@ struct Enc {
     const PairT* mdp;         // the current position's pairs (packed): its ring slot, or md_buf
     PairT* md_buf;            // a copy when the list is longer than the inline pairs or is clamped
     PairT* md_buf_alt;        // W2: the other position's md_buf
+    uint8_t* win;             // gather window: the cur side's bytes at offsets -1 .. kGW - 2 (aliased by tp)
+    uint8_t* win_alt;         // W2: the other position's gather window
     uint8_t* lds_base;        // W2: LDS offsets in the hand-off
     Pipe* pipe;               // W2: the hand-off record
     uint32_t* ring_info;      // [kRing]
@@ -408,10 +411,11 @@ struct Enc {
     // o = -1 .. kGW-2 from p (the current byte) on the cur side and at
     // p + o - dist - 1 on the rep / match sides. gather() issues all of those
     // byte loads at once (one lane per offset, one memory round trip), keeps
-    // equality masks per side (bit o+1 = bytes equal at offset o) and keeps the
-    // three bytes the position step prices its literal with in scalars. Compares
-    // past the window fall back to match_len.
+    // equality masks per side (bit o+1 = bytes equal at offset o), keeps the three
+    // bytes the position step prices its literal with in scalars and the cur side's
+    // bytes in LDS (two-step literals). Compares past the window fall back to match_len.
     FI void gather(bool with_pairs) {
+        if (W2) { uint8_t* t = win; win = win_alt; win_alt = t; }   // B may still read the last position's bytes
         gp = mfpos - 1;
         const uint32_t d0 = rp0 + 1, d1 = rp1 + 1, d2 = rp2 + 1, d3 = rp3 + 1;
         const uint32_t e0 = num_pairs > 0 ? md_d(0) + 1 : d0, e1 = num_pairs > 1 ? md_d(1) + 1 : d0;
@@ -436,6 +440,8 @@ struct Enc {
                 gmp0 |= (uint64_t)wballot(va[it] == w0[it]) << sh;
                 gmp1 |= (uint64_t)wballot(va[it] == w1[it]) << sh;
             }
+            win[k] = (uint8_t)va[it];   // the cur side only: the other sides' bytes are read (rarely, by a
+                                         // two-step candidate's literal) straight from the stream
         }
         // the three bytes every position step reads, straight from the loaded registers
         // (offsets -1 and 0 are window entries 0 and 1): no LDS round trip on the chain
@@ -445,9 +451,10 @@ struct Enc {
         LANE_FENCE();
     }
     // byte at p + o on the cur side
-    // only a two-step candidate's literal (a few percent of the positions) reads one: from the
-    // stream (the gather keeps no bytes in LDS)
-    FI uint32_t a_byte(int32_t o) const { return in_byte(gp + (uint32_t)o); }
+    // byte at p + o on the cur side (a two-step candidate's literal)
+    FI uint32_t a_byte(int32_t o) const {
+        return (o >= -1 && o <= kGW - 2) ? (uint32_t)win[o + 1] : in_byte(gp + (uint32_t)o);
+    }
     // byte at p + o - dist - 1 (side 1..6 = rep0..3, pair0..1; side < 0: not gathered); only a
     // two-step candidate's literal reads one (a few percent of the positions): from the stream
     FI uint32_t b_byte(int side, uint32_t dist, int32_t o) const {
@@ -1181,7 +1188,7 @@ struct Enc {
     }
     // N: slot cur + 1's literal and short-rep candidates (nx_*: its fields, read by the caller)
     template <bool F>
-    FI bool pos_next_part(uint32_t cur, const PosS& r, uint32_t nx_price, uint32_t nx_pp, int32_t nx_bp, uint32_t nx_fs,
+    FI bool pos_next_part(uint32_t cur, const PosS& r, uint32_t nx_price, uint32_t nx_pp, int32_t nx_bp,
                           uint32_t& match_price, uint32_t& rep_match_price) {
         constexpr bool FA = F || RING;
         PBEGIN(tn);
@@ -1189,7 +1196,7 @@ struct Enc {
         bool next_is_char = false;
         if (r.cur_and1 < nx_price) {
             nx_price = r.cur_and1; nx_pp = (nx_pp & 0xFFFF0000u) | cur; nx_bp = -1;
-            set_price<FA>(nx, nx_price); set_pp<FA>(nx, nx_pp); set_bp<FA>(nx, -1); set_fs<FA>(nx, nx_fs & ~1u);
+            set_price<FA>(nx, nx_price); set_pp<FA>(nx, nx_pp); set_bp<FA>(nx, -1); set_fs<FA>(nx, fs_at<FA>(nx) & ~1u);
             next_is_char = true;
         }
         match_price = r.cur_price + dm1(E_IS_MATCH + (st << PBS) + pos_state);
@@ -1197,7 +1204,7 @@ struct Enc {
         if (r.match_byte == r.cur_byte && !((nx_pp & 0xFFFFu) < cur && nx_bp == 0)) {
             uint32_t srp = rep_match_price + rep_len1_price(st, pos_state);
             if (srp <= nx_price) {
-                set_price<FA>(nx, srp); set_pp<FA>(nx, (nx_pp & 0xFFFF0000u) | cur); set_bp<FA>(nx, 0); set_fs<FA>(nx, nx_fs & ~1u);
+                set_price<FA>(nx, srp); set_pp<FA>(nx, (nx_pp & 0xFFFF0000u) | cur); set_bp<FA>(nx, 0); set_fs<FA>(nx, fs_at<FA>(nx) & ~1u);
                 next_is_char = true;
             }
         }
@@ -1212,10 +1219,10 @@ struct Enc {
         // cur + 1's slot: nothing before its literal / short-rep update below writes it, so its
         // reads are issued before the gather and complete under the gather's memory round trip
         const uint32_t nx = cur + 1;
-        const uint32_t nx_price = price_at<FA>(nx), nx_pp = pp_at<FA>(nx), nx_fs = fs_at<FA>(nx);
+        const uint32_t nx_price = price_at<FA>(nx), nx_pp = pp_at<FA>(nx);
         const int32_t nx_bp = bp_at<FA>(nx);
         pos_gather_part<F>(cur, position, r);
-        return pos_next_part<F>(cur, r, nx_price, nx_pp, nx_bp, nx_fs, match_price, rep_match_price);
+        return pos_next_part<F>(cur, r, nx_price, nx_pp, nx_bp, match_price, rep_match_price);
     }
 
     // R: the rest of position cur's step (Encoder.java:743-808): the literal + rep0
@@ -1409,6 +1416,7 @@ struct Enc {
             P->new_len = new_len; P->npairs = npairs;
             P->gp = gp; P->mfpos = mfpos;
             P->md_off = (uint32_t)((const uint8_t*)mdp - lds_base); P->mdbuf_off = (uint32_t)((uint8_t*)md_buf - lds_base);
+            P->win_off = (uint32_t)(win - lds_base);
             P->rp0 = rp0; P->rp1 = rp1; P->rp2 = rp2; P->rp3 = rp3;
             P->gm0 = gm0; P->gm1 = gm1; P->gm2 = gm2; P->gm3 = gm3; P->gmp0 = gmp0; P->gmp1 = gmp1;
         }
@@ -1479,10 +1487,10 @@ struct Enc {
             new_len = nnew;
             // N(cur): slot cur + 1, now that R(cur - 1) is done
             const uint32_t nx = cur + 1;
-            const uint32_t nx_price = price_at<true>(nx), nx_pp = pp_at<true>(nx), nx_fs = fs_at<true>(nx);
+            const uint32_t nx_price = price_at<true>(nx), nx_pp = pp_at<true>(nx);
             const int32_t nx_bp = bp_at<true>(nx);
-            if (nx < (uint32_t)kOptLds) { pos_commit<true>(cur, nr); next_is_char = pos_next_part<true>(cur, nr, nx_price, nx_pp, nx_bp, nx_fs, match_price, rep_match_price); }
-            else { pos_commit<false>(cur, nr); next_is_char = pos_next_part<false>(cur, nr, nx_price, nx_pp, nx_bp, nx_fs, match_price, rep_match_price); }
+            if (nx < (uint32_t)kOptLds) { pos_commit<true>(cur, nr); next_is_char = pos_next_part<true>(cur, nr, nx_price, nx_pp, nx_bp, match_price, rep_match_price); }
+            else { pos_commit<false>(cur, nr); next_is_char = pos_next_part<false>(cur, nr, nx_price, nx_pp, nx_bp, match_price, rep_match_price); }
             r = nr;
             publish(kPipeRelax, cur, position, r, next_is_char, match_price, rep_match_price, new_len, num_pairs, len_end);
             pipe_sync();   // Q: B runs R(cur)
@@ -1507,6 +1515,7 @@ struct Enc {
             gp = P->gp; mfpos = P->mfpos;
             mdp = (const PairT*)(lds_base + P->md_off);
             md_buf = (PairT*)(lds_base + P->mdbuf_off);
+            win = lds_base + P->win_off;
             rp0 = P->rp0; rp1 = P->rp1; rp2 = P->rp2; rp3 = P->rp3;
             gm0 = P->gm0; gm1 = P->gm1; gm2 = P->gm2; gm3 = P->gm3; gmp0 = P->gmp0; gmp1 = P->gmp1;
             uint32_t len_end = P->len_end;
@@ -1672,7 +1681,7 @@ struct Enc {
 // LDS layout of one stream's workgroup; shared by the kernel (carving) and
 // the host (dynamic LDS size). Regions are 16-byte aligned.
 enum { L_PP, L_PROBS, L_DMP, L_LENP, L_LENC, L_PSP, L_DP, L_AP, L_TP, L_MDBUF, L_RINFO, L_RPAIRS, L_OPRICE,
-       L_OPP, L_OBP, L_OBP2, L_OFS, L_OBACKS, L_OBYTES, L_TPBUF, L_RBUF, L_LIT, L_PIPE, L_MDBUF2, L_COUNT };
+       L_OPP, L_OBP, L_OBP2, L_OFS, L_OBACKS, L_OBYTES, L_TPBUF, L_RBUF, L_LIT, L_PIPE, L_MDBUF2, L_WIN2, L_COUNT };
 __host__ __device__ inline uint32_t enc_lds_layout(const EncArgs& a, uint32_t* off) {
     const uint32_t md_cap = a.fb + 2;   // pairs per position <= fb (+1 clamp slot)
     const uint32_t sz[L_COUNT] = {
@@ -1681,7 +1690,7 @@ __host__ __device__ inline uint32_t enc_lds_layout(const EncArgs& a, uint32_t* o
         (a.w2 ? 2u : 1u) * kRing * kInlinePairs * a.pair_bytes,
         (kOptLds + 2) * 4, (kOptLds + 2) * 4, (kOptLds + 2) * 4, (kOptLds + 2) * 4, kOptLds + 2, 4 * kOptLds * 4, kOptLds * 4, kTpBytes, kRbuf * 2 + 2,
         a.lit_in_lds ? (0x300u << (a.lc + a.lp)) * 2 + 2 : 0u,
-        a.w2 ? (uint32_t)sizeof(Pipe) : 0u, a.w2 ? md_cap * a.pair_bytes : 0u};
+        a.w2 ? (uint32_t)sizeof(Pipe) : 0u, a.w2 ? md_cap * a.pair_bytes : 0u, a.w2 ? (uint32_t)kGW : 0u};
     uint32_t o = 0;
     for (int i = 0; i < L_COUNT; i++) { if (off) off[i] = o; o += (sz[i] + 15) & ~15u; }
     return o;
@@ -1721,7 +1730,8 @@ __global__ void __launch_bounds__(W2 ? 2 * kWave : kWave, W2 ? 2 : 4) enc_kernel
     e.psp = (uint16_t*)(smem + off[L_PSP]);
     e.dp = (uint16_t*)(smem + off[L_DP]);
     e.ap = (uint32_t*)(smem + off[L_AP]);
-    e.tp = (uint16_t*)(smem + off[L_TPBUF]);   // tempPrices (FillDistancesPrices' scratch)
+    e.tp = (uint16_t*)(smem + off[L_TPBUF]);   // tempPrices (FillDistancesPrices' scratch), aliasing the window
+    e.win = smem + off[L_TPBUF];
     e.dmp = (uint32_t*)(smem + off[L_DMP]);
     e.md_buf = (PairT*)(smem + off[L_MDBUF]);
     e.mdp = e.md_buf;
@@ -1739,6 +1749,7 @@ __global__ void __launch_bounds__(W2 ? 2 * kWave : kWave, W2 ? 2 : 4) enc_kernel
         e.lds_base = smem;
         e.pipe = (Pipe*)(smem + off[L_PIPE]);
         e.md_buf_alt = (PairT*)(smem + off[L_MDBUF2]);
+        e.win_alt = smem + off[L_WIN2];
     }
     uint8_t* scratch = a.scratch + (size_t)blockIdx.x * a.scratch_stride;
     e.spill = __builtin_amdgcn_make_buffer_rsrc(scratch, 0, kNumOpts * 4 * 10, 0x00020000);
