@@ -89,6 +89,9 @@ def parse():
                          "when that decode is done, lzma_ctx_set_parse_fence)")
     ap.add_argument("--emulate", action="store_true",
                     help="CPU tests only: CPU tensors, gloo and the SIMT-emulated product kernels (measures nothing)")
+    ap.add_argument("--project-share", type=int, default=1,
+                    help="PROJECTION (one GPU, no process group): time rank 0's share of the buffer dealt over G "
+                         "GPUs; value = the buffer's bytes / that share's step time (the G-GPU run is the driver's)")
     ap.add_argument("--dump-container", default=None,
                     help="rank 0 writes the gathered multi-member container of the strong pass to this path")
     return ap.parse_args()
@@ -180,8 +183,9 @@ def run_pass(args, D, p, ctxs, strong, rank, world, dist):
     size = full.size
     n_all = (size + args.chunk - 1) // args.chunk
     all_offs = np.minimum(np.arange(n_all + 1, dtype=np.uint64) * np.uint64(args.chunk), np.uint64(size))
-    mine = lzdist.rank_streams(n_all, rank, world) if strong else np.arange(n_all)
-    if strong and world > 1:
+    deal = max(world, args.project_share)   # --project-share: rank 0's share of a G-way deal, on one GPU
+    mine = lzdist.rank_streams(n_all, rank, deal) if strong else np.arange(n_all)
+    if strong and deal > 1:
         host = np.concatenate([full[int(all_offs[i]):int(all_offs[i + 1])] for i in mine]) if mine.size else full[:0]
     else:
         host = full
@@ -444,6 +448,7 @@ def main():
                               "oracle's Encoder.Code restatement%s" % (
                                   "; rank 0's gathered container holds every stream" if dist else ""),
             "parity_streams_checked": checked, "roundtrip_ok": r["roundtrip"],
+            "projection_of_n_gpus": args.project_share if args.project_share > 1 else None,
             "gathered": r["gathered"], "weak_scaling": weak,
             "kernels_ms": {k: {"total_ms": v[0], "launches": v[1]} for k, v in timings.items()},
             "roofline": roofline, "cpu_baseline": cpu, "single_stream": single,
