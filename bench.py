@@ -468,12 +468,16 @@ def main():
 _KERNEL_OF = {"enc_parse": "enc_kernel", "dec_stream": "dec_kernel", "mf_walk": "mf_walk_kernel"}
 
 
+def _profile_prefix(wl):
+    """config 3 (TEXT) has its own summaries (round 3, tools/r03_text.sh); the bench
+    workload's are round 4's (tools/r04/prof.sh)"""
+    return "r03/text_" if wl.get("data") == "text" else "r04/"
+
+
 def _profile(name, wl):
     """A committed per-kernel summary from profiles/ (written by tools/profile_round.sh
     over this same workload), or None when absent or taken on another workload."""
-    if wl.get("data") == "text":   # config 3's own summaries (tools/profile_r03.sh text)
-        name = "r03/text_" + name
-    path = os.path.join(REPO, "profiles", name)
+    path = os.path.join(REPO, "profiles", _profile_prefix(wl) + name)
     if not os.path.exists(path):
         return None
     with open(path) as f:
@@ -496,7 +500,7 @@ def pmc_traffic(label, wl):
     for k, v in t.items():
         if k.startswith(prefix) and isinstance(v, dict) and "traffic_bytes_per_launch" in v:
             return v["traffic_bytes_per_launch"], "profiles/%straffic.json (%s, rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)" % (
-                "r03/text_" if wl.get("data") == "text" else "", k)
+                _profile_prefix(wl), k)
     return None, None
 
 
@@ -517,7 +521,7 @@ def issue_bound(label, wl, avg_s, nbytes):
                 v.get("SQ_INSTS_VMEM", 0) + v.get("SQ_INSTS_SMEM", 0) + v.get("SQ_INSTS_BRANCH", 0)
             return {"salu_per_cu": salu / cus, "salu_issue_frac": salu / cus / (clk * avg_s) if avg_s > 0 else None,
                     "salu_per_input_byte": salu / max(nbytes, 1), "insts_per_input_byte": insts / max(nbytes, 1),
-                    "clock_hz": clk, "source": "profiles/issue.json (%s)" % k}
+                    "clock_hz": clk, "source": "profiles/%sissue.json (%s)" % (_profile_prefix(wl), k)}
     return None
 
 
