@@ -86,7 +86,11 @@ def parse():
     ap.add_argument("--sequential", action="store_true",
                     help="run each step's encode and decode back to back (default: pipelined, step k's decode on "
                          "its own HIP stream and context beside step k+1's match finder; step k+1's parser starts "
-                         "when that decode is done, lzma_ctx_set_parse_fence)")
+                         "when that decode is done, lzma_ctx_set_parse_fence; see --pipeline)")
+    ap.add_argument("--pipeline", choices=["split", "decode"], default="decode",
+                    help="pipelined schedule: decode (default) = step k's pack + decode beside step k+1's match "
+                         "finder, with the synchronous encode; split = the split encode, step k's range coder "
+                         "beside them too (measured the same: profiles/r04/ab_bench_split_encode_vs_decode_overlap.jsonl)")
     ap.add_argument("--emulate", action="store_true",
                     help="CPU tests only: CPU tensors, gloo and the SIMT-emulated product kernels (measures nothing)")
     ap.add_argument("--project-share", type=int, default=1,
@@ -224,11 +228,27 @@ def run_pass(args, D, p, ctxs, strong, rank, world, dist):
         if state.pop("dec_inflight", False):
             check_dec(*ctx_dec.decode_batch_dev_wait())
 
-    def step(k):
+    def step(k, nxt):
         t0 = time.perf_counter()
-        lens = ctx.encode_batch_dev(d_in, offs, p, d_comp, cap_offs, st)
         buf = d_packs[k % 2]
-        pk = ctx.pack_dev(d_comp, cap_offs, lens, buf, st)   # synchronous: buf is complete
+        if overlap and args.pipeline == "split":
+            # the split encode: step k's walk and parser on st (the parser after step k-1's
+            # decode), its range coder on the encoder context's coder stream; step k+1's
+            # match finder is staged behind the parser and runs beside that coder and
+            # beside step k's pack + decode (decoder context, st_dec)
+            if not state.get("staged"):
+                ctx.encode_stage_dev(d_in, offs, p, d_comp, cap_offs, st)
+            ctx.encode_parse_dev_async(st)
+            state["staged"] = nxt
+            if nxt:
+                ctx.encode_stage_dev(d_in, offs, p, d_comp, cap_offs, st)
+            lens = ctx.encode_parse_dev_wait()
+            join()   # step k-1's decode: done (step k's parser waited for it)
+            pk = ctx_dec.pack_dev(d_comp, cap_offs, lens, buf, st_dec)   # synchronous: buf is complete
+        else:
+            lens = ctx.encode_batch_dev(d_in, offs, p, d_comp, cap_offs, st)
+            join()
+            pk = ctx.pack_dev(d_comp, cap_offs, lens, buf, st)   # synchronous: buf is complete
         if dist:   # the single data exchange: rank 0 collects every rank's packed streams
             g, all_lens, counts = lzdist.gather_streams(buf, lens, dst=0)
             state["gathered"] = None if g is None else (g, all_lens, counts)
@@ -242,8 +262,10 @@ def run_pass(args, D, p, ctxs, strong, rank, world, dist):
             torch.distributed.barrier()
         D.sync()
 
+    # every step stages the next one inside its own time; the last step of each loop
+    # stages nothing, so the timed loop holds exactly its own steps' work
     for k in range(args.warmup):
-        step(k)
+        step(k, k + 1 < args.warmup)
     join()
     for c in (ctx, ctx_dec):
         c.set_timing(True)
@@ -252,7 +274,7 @@ def run_pass(args, D, p, ctxs, strong, rank, world, dist):
     barrier()
     t0 = time.perf_counter()
     for k in range(args.steps):
-        step(k)
+        step(k, k + 1 < args.steps)
     join()
     barrier()
     elapsed = time.perf_counter() - t0
@@ -440,9 +462,11 @@ def main():
             "decompress_MBps": size * args.steps / max(t_dec, 1e-9) / 1e6,
             "schedule": ("sequential: each step's encode and decode back to back; compress/decompress MB/s are "
                          "each phase's wall time (rank 0)") if args.sequential else
-                        ("pipelined: step k's decode (own context + HIP stream) runs beside step k+1's match finder, "
-                         "step k+1's parser waits for it; compress/decompress MB/s are each phase's summed kernel "
-                         "times (HIP events), which overlap"),
+                        ("pipelined (%s): step k's %sdecode (own context + HIP stream) runs beside step k+1's "
+                         "match finder, step k+1's parser waits for the decode; compress/decompress MB/s are each "
+                         "phase's summed kernel times (HIP events), which overlap" % (
+                             args.pipeline, "range coder (the encoder's coder stream), pack and "
+                             if args.pipeline == "split" else "")),
             "ratio": ratio, "chunking": chunking, "verified": ok,
             "verified_means": "every stream decodes to its input and every sampled stream's bytes equal the "
                               "oracle's Encoder.Code restatement%s" % (

@@ -89,6 +89,29 @@ int lzma_enc_batch_dev(lzma_ctx *ctx, const lzma_params *p,
  * (nstreams+1 entries): packs capacity-layout encoder output. */
 int lzma_pack_dev(lzma_ctx *ctx, const uint8_t *d_src, const uint64_t *h_src_offs, const uint64_t *h_lens,
                   int nstreams, uint8_t *d_dst, const uint64_t *h_dst_offs, void *hip_stream);
+/* The same encode in three calls, for a caller that pipelines batches: the range
+ * coder of one batch runs on the context's own coder stream while the next batch's
+ * match finder runs on the caller's stream.
+ *   lzma_enc_stage_dev: stages the batch (arguments as lzma_enc_batch_dev; d_in and
+ *     d_out must stay valid until _wait) and enqueues its match finder's keys, sorts
+ *     and chain lists on hip_stream; returns without waiting.
+ *   lzma_enc_parse_dev_async: the walk (it reads the chain count and the walk's
+ *     verdict back: waits for the match finder), then the parser on hip_stream (after
+ *     the parse fence's decode, if any), then the range coder on the coder stream;
+ *     returns without waiting for the parser or the coder.
+ *   lzma_enc_parse_dev_wait: waits for the coder; h_out_lens as lzma_enc_batch_dev.
+ * One pass only: at most 16384 streams and lzma_ctx_set_batch_bytes of input
+ * (LZMA_E_PARAM otherwise). Order: stage, parse_async, then either wait or the next
+ * batch's stage (it may run while the coder is in flight) followed by wait; a second
+ * parse_async before wait returns LZMA_E_PARAM. While a batch is staged or its coder
+ * is in flight, the context's other encode, decode and pack entry points return
+ * LZMA_E_PARAM. Reference: Encoder.Code (Encoder.java:1064-1077), as for
+ * lzma_enc_batch_dev; the bytes are the same. */
+int lzma_enc_stage_dev(lzma_ctx *ctx, const lzma_params *p,
+                       const uint8_t *d_in, const uint64_t *h_offs, int nstreams,
+                       uint8_t *d_out, const uint64_t *h_out_offs, void *hip_stream);
+int lzma_enc_parse_dev_async(lzma_ctx *ctx, void *hip_stream);
+int lzma_enc_parse_dev_wait(lzma_ctx *ctx, uint64_t *h_out_lens);
 /* Host buffers: out is packed, out_offs[nstreams+1] receives the layout. */
 int lzma_enc_batch(lzma_ctx *ctx, const lzma_params *p,
                    const uint8_t *in, const uint64_t *offs, int nstreams,

@@ -598,12 +598,7 @@ static inline unsigned grid_for(uint64_t n, unsigned block, unsigned cap = 65536
     return (unsigned)(g < cap ? g : cap);
 }
 
-// Runs K1..K4 for one batch. in: padded device copy of the batch; offs: device
-// stream offsets (nstreams+1). Fills w.pairs (records) / w.ovf_off / w.ovf.
-int run_match_finder(Ctx* ctx, const Derived& d, const uint8_t* in, const uint64_t* d_offs, int nstreams,
-                     uint64_t total, bool wide_pairs, MfBuffers& w, hipStream_t st) {
-    if (total == 0) return LZMA_OK;
-    if (total >= 0xFFFFFFFFull) return ctx->fail(LZMA_E_PARAM, "batch too large for 32-bit positions");
+static MfArgs mf_args(const Derived& d, const MfBuffers& w, uint64_t total, int nstreams, bool wide_pairs) {
     MfArgs a{};
     a.fb = d.fb; a.min_match_check = d.min_match_check; a.hash_mask = d.hash_mask; a.hash_bits = d.hash_bits;
     a.cut_value = d.cut_value; a.cyc_size = d.cyc_size; a.direct_bytes = d.direct_bytes;
@@ -614,6 +609,25 @@ int run_match_finder(Ctx* ctx, const Derived& d, const uint8_t* in, const uint64
         if (sscanf(e, "%u,%u", &lo, &hi) >= 1) { a.walk_lo = lo; a.walk_hi = hi; }
     }
     a.k4 = w.k4; a.k3 = (uint32_t*)w.k3; a.k2 = (uint32_t*)w.k2; a.vals = w.vals; a.mrec = w.pairs; a.rec_vecs = wide_pairs ? rec_vecs<uint64_t>() : rec_vecs<uint32_t>(); a.prev2 = w.prev2; a.prev3 = w.prev3;
+    return a;
+}
+
+// K1..K4 for one batch, in two calls. in: padded device copy of the batch; offs: device
+// stream offsets (nstreams+1). mf_front enqueues the keys, sorts and chain lists and
+// returns; mf_back reads the chain count back (one host round trip), runs the walk and
+// reads its verdict back. Fills w.pairs (records) / w.ovf_off / w.ovf.
+// The long chains' scratch list: k4, dead since the hash4 sort (mf_chains_kernel fills it)
+static uint32_t mf_long_min() {
+    // LZG_WALK_LONG overrides the long-chain threshold (experiments; 4294967295 = stream order only)
+    static const uint32_t long_min = getenv("LZG_WALK_LONG") ? (uint32_t)strtoul(getenv("LZG_WALK_LONG"), nullptr, 10) : kWalkLong;
+    return long_min;
+}
+
+int mf_front(Ctx* ctx, const Derived& d, const uint8_t* in, const uint64_t* d_offs, int nstreams, uint64_t total,
+             bool wide_pairs, MfBuffers& w, hipStream_t st) {
+    if (total == 0) return LZMA_OK;
+    if (total >= 0xFFFFFFFFull) return ctx->fail(LZMA_E_PARAM, "batch too large for 32-bit positions");
+    MfArgs a = mf_args(d, w, total, nstreams, wide_pairs);
     const bool bt4 = d.hash_array != 0;
     const unsigned B = 256;
     {
@@ -647,8 +661,7 @@ int run_match_finder(Ctx* ctx, const Derived& d, const uint8_t* in, const uint64
     uint32_t* okey = (uint32_t*)w.k2;
     uint32_t* okey_sorted = (uint32_t*)w.k3;
     uint32_t* long_raw = (uint32_t*)w.k4;   // dead since the hash4 sort
-    // LZG_WALK_LONG overrides the long-chain threshold (experiments; 4294967295 = stream order only)
-    static const uint32_t long_min = getenv("LZG_WALK_LONG") ? (uint32_t)strtoul(getenv("LZG_WALK_LONG"), nullptr, 10) : kWalkLong;
+    const uint32_t long_min = mf_long_min();
     {
         TimedLaunch tl(ctx, "mf_sort", st);
         hipMemsetAsync(w.cls, 0, 96 * sizeof(uint32_t), st);
@@ -659,6 +672,17 @@ int run_match_finder(Ctx* ctx, const Derived& d, const uint8_t* in, const uint64
         if ((rc = seg_radix_sort(ctx, false, okey, w.chain_idx, okey_sorted, w.chain_order, w.son, w.son + total, w.hist, total,
                                  d_offs, nstreams, 8, st, w.seg_end, w.chain_offs))) return rc;
     }
+    return LZMA_OK;
+}
+
+int mf_back(Ctx* ctx, const Derived& d, const uint8_t* in, const uint64_t* d_offs, int nstreams, uint64_t total,
+            bool wide_pairs, MfBuffers& w, hipStream_t st) {
+    if (total == 0) return LZMA_OK;
+    MfArgs a = mf_args(d, w, total, nstreams, wide_pairs);
+    const bool bt4 = d.hash_array != 0;
+    const unsigned B = 256;
+    uint32_t* long_raw = (uint32_t*)w.k4;
+    const uint32_t long_min = mf_long_min();
     // sizes the walk grid: one host round trip per pass (pinned: see HostBuf)
     if (!ctx->pin_mf.ensure(16)) return ctx->fail(LZMA_E_NOMEM, "pinned staging");
     uint64_t* p_cnt = ctx->pin_mf.as<uint64_t>();

@@ -115,6 +115,8 @@ struct HostBuf {
     template <typename T> T* as(size_t byte_off = 0) const { return (T*)((uint8_t*)p + byte_off); }
 };
 
+struct EncPass;   // runtime.hip: one encode pass in pieces
+
 struct Ctx {
     uint32_t magic = kCtxMagic;   // first member: see kCtxMagic
     int device = 0;
@@ -141,6 +143,15 @@ struct Ctx {
     // parse fence (lzma_ctx_set_parse_fence): an encode pass waits for this
     // context's decode in flight before it launches its parser
     const Ctx* fence = nullptr;
+    // split encode (lzma_enc_stage_dev -> lzma_enc_parse_dev_async -> lzma_enc_parse_dev_wait):
+    // the staged pass, and the range coder in flight on the context's coder stream
+    EncPass* split_pass = nullptr;
+    int split_state = 0;                   // 0 idle, 1 staged, 2 parsed (coder in flight)
+    int rc_pending = 0;                    // streams of the coder in flight
+    hipEvent_t rc_done = nullptr, parse_done = nullptr;
+    hipStream_t rc_stream = nullptr;       // created on first use
+    DevBuf split_recs, split_coder;        // the coder's records and per-stream arrays (apart from the arena)
+    HostBuf pin_rc;                        // the coder's lengths and verdicts
     // timing
     bool timing = false;
     struct Pending { std::string name; hipEvent_t a, b; };
@@ -286,8 +297,10 @@ __global__ void iota_kernel(uint32_t* out, uint64_t n);
 // fb - 1 pairs per position: lengths 2..fb, strictly increasing)
 __host__ __device__ inline uint32_t ovf_stride(uint32_t fb) { return fb > (uint32_t)kInlinePairs + 1 ? fb - 1 - kInlinePairs : 1u; }
 
-int run_match_finder(Ctx* ctx, const Derived& d, const uint8_t* in, const uint64_t* d_offs, int nstreams,
-                     uint64_t total, bool wide_pairs, MfBuffers& w, hipStream_t st);
+int mf_front(Ctx* ctx, const Derived& d, const uint8_t* in, const uint64_t* d_offs, int nstreams, uint64_t total,
+             bool wide_pairs, MfBuffers& w, hipStream_t st);
+int mf_back(Ctx* ctx, const Derived& d, const uint8_t* in, const uint64_t* d_offs, int nstreams, uint64_t total,
+            bool wide_pairs, MfBuffers& w, hipStream_t st);
 // sort.hip: stable per-stream radix sort by the low end_bit key bits
 int seg_radix_sort(Ctx* ctx, bool key64, const void* kin, const uint32_t* vin, void* kout, uint32_t* vout,
                    uint64_t* tmp_a, uint64_t* tmp_b, uint32_t* hist, uint64_t n, const uint64_t* d_offs, int nstreams,

@@ -105,201 +105,298 @@ struct MatchDump {
     uint32_t stride = 0;
 };
 
-// one encode pass over streams [s0, s1) of a batch (dump != null: stop after
-// the match finder and copy its output to the host)
+// One encode pass over streams [s0, s1) of a batch, in pieces: plan (host arrays),
+// carve (the arena layout), stage (input and offsets to the device), the match
+// finder's front (keys, sorts, chain lists: enqueued only) and back (the walk; reads
+// the chain count and the walk's verdict back), the parser, the range coder. The
+// synchronous entry points run them back to back on one HIP stream (encode_pass);
+// the split form (lzma_enc_stage_dev / lzma_enc_parse_dev_async / _wait) runs the
+// range coder on the context's coder stream, out of buffers no later pass touches
+// while it runs, so a pipelined caller overlaps it with the next batch's match finder.
+struct EncPass {
+    Derived d{};
+    const uint8_t* d_in = nullptr;
+    uint8_t* d_out = nullptr;
+    int ns = 0;
+    uint64_t in0 = 0, total = 0;
+    bool wide = false, split = false;
+    size_t psz = 4;
+    std::vector<uint64_t> offs, oofs, rofs;
+    std::vector<uint32_t> order;
+    int grid = 0;
+    size_t scr = 0;
+    uint64_t stride = 0, slots_per_k = 64, ovf_cap = 0;
+    MfBuffers w{};
+    uint8_t *inpad = nullptr, *d_scr = nullptr;
+    uint64_t *d_offs = nullptr, *d_oofs = nullptr, *d_lens = nullptr, *d_rofs = nullptr, *d_rlens = nullptr;
+    uint32_t *d_order = nullptr, *d_seg = nullptr;
+    int32_t* d_status = nullptr;
+    unsigned* d_next = nullptr;
+    uint16_t* d_recs = nullptr;
+    uint64_t pool_cap(uint64_t spk) const {   // one slot per position at most
+        uint64_t slots = std::min<uint64_t>(total, (total * spk + 1023) / 1024) + 64;
+        return slots * stride;
+    }
+};
+
+static void pass_plan(Ctx* ctx, EncPass& P, const Derived& d, const uint8_t* d_in, const uint64_t* h_offs, int s0, int s1,
+                      uint8_t* d_out, const uint64_t* h_out_offs, bool split) {
+    P.d = d;
+    P.d_in = d_in;
+    P.d_out = d_out;
+    P.split = split;
+    P.ns = s1 - s0;
+    const int ns = P.ns;
+    P.in0 = h_offs[s0];
+    P.total = h_offs[s1] - P.in0;
+    P.offs.assign(ns + 1, 0);
+    P.oofs.assign(ns + 1, 0);
+    for (int i = 0; i <= ns; i++) { P.offs[i] = h_offs[s0 + i] - P.in0; P.oofs[i] = h_out_offs[s0 + i]; }
+    P.wide = false;
+    for (int i = 0; i < ns; i++)
+        if (P.offs[i + 1] - P.offs[i] >= PairPack<uint32_t>::kMaxStream) P.wide = true;
+    P.psz = P.wide ? 8 : 4;
+    // longest streams first (work queue order)
+    P.order.resize(ns);
+    std::iota(P.order.begin(), P.order.end(), 0u);
+    std::stable_sort(P.order.begin(), P.order.end(), [&](uint32_t a, uint32_t b) {
+        return (P.offs[a + 1] - P.offs[a]) > (P.offs[b + 1] - P.offs[b]);
+    });
+    P.grid = enc_grid(d, ns);
+    P.scr = (enc_scratch_per_block(d) + 255) & ~(size_t)255;
+    // overflow pool in slots of ovf_stride(fb) pairs, one slot per position with more
+    // than kInlinePairs pairs: start at 1 slot per 16 positions (a retry grows it 4x and
+    // remembers the rate for later passes of this context), never more than one per position
+    P.stride = ovf_stride(d.fb);
+    P.slots_per_k = std::max<uint64_t>(64, ctx->ovf_hint);
+    P.ovf_cap = P.pool_cap(P.slots_per_k);
+    // coder records (rc.hip) per stream: capacity layout in records, 64-record aligned
+    P.rofs.assign(ns + 1, 0);
+    for (int i = 0; i < ns; i++) P.rofs[i + 1] = P.rofs[i] + rc_record_bound(P.offs[i + 1] - P.offs[i]);
+}
+
+// The arena layout for the pass's current overflow pool. The sync form keeps the coder
+// records in the memory of the match finder's buffers (dead after the walk); the split
+// form keeps them, and the coder's own arrays, in separate allocations (Ctx::split_*)
+// that the next pass's match finder never touches.
+static int pass_carve(Ctx* ctx, EncPass& P) {
+    const uint64_t T = P.total;
+    const int ns = P.ns;
+    auto phase1 = [&](Carver& c, MfBuffers& w) {   // buffers only the match finder uses
+        w.k4 = c.take<uint64_t>(T); w.k3 = c.take<uint64_t>(T); w.k2 = c.take<uint64_t>(T); w.ks = c.take<uint64_t>(T);
+        w.vals = c.take<uint32_t>(T); w.vs = c.take<uint32_t>(T);
+        w.prev2 = c.take<uint32_t>(T); w.prev3 = c.take<uint32_t>(T);
+        w.flag = c.take<uint8_t>(T);
+        w.chain_start = c.take<uint32_t>(T); w.chain_len = c.take<uint32_t>(T); w.long_list = c.take<uint32_t>(T);
+        w.chain_idx = c.take<uint32_t>(T); w.chain_order = c.take<uint32_t>(T);
+        w.cls = c.take<uint32_t>(96);
+        w.son = c.take<uint64_t>(4 * T);   // mf.hip WNode: 32 bytes per position
+        w.hist = c.take<uint32_t>((size_t)ns * 1024);
+        w.seg_end = c.take<uint64_t>((size_t)ns + 1);
+        w.chain_offs = c.take<uint64_t>((size_t)ns + 1);
+    };
+    size_t p1_bytes;
+    {
+        MfBuffers pw{};
+        Carver probe(nullptr);
+        phase1(probe, pw);
+        p1_bytes = probe.off;
+    }
+    const size_t rec_bytes_all = P.rofs[ns] * 2;
+    const size_t union_bytes = P.split ? p1_bytes : std::max<size_t>(p1_bytes, rec_bytes_all);
+    auto need = [&](Carver& c, EncPass& Q) {
+        Q.inpad = c.take<uint8_t>(T + 512);
+        Q.d_offs = c.take<uint64_t>(ns + 1);
+        Q.d_oofs = c.take<uint64_t>(ns + 1);
+        Q.d_order = c.take<uint32_t>(ns);
+        Q.d_lens = c.take<uint64_t>(ns);
+        Q.d_status = c.take<int32_t>(ns);
+        Q.d_next = c.take<unsigned>(4);
+        Q.d_rofs = c.take<uint64_t>(ns + 1);
+        Q.d_rlens = c.take<uint64_t>(ns);
+        Q.d_seg = c.take<uint32_t>((size_t)ns * kRcSegs * kRcSegWords);
+        uint8_t* u = c.take<uint8_t>(union_bytes);
+        Q.d_recs = (uint16_t*)u;
+        Carver c1(u);
+        phase1(c1, Q.w);
+        Q.w.pairs = (v4u32*)c.take<uint8_t>(T * rec_bytes(Q.wide));
+        Q.w.ovf_off = c.take<uint32_t>(T);
+        Q.w.ovf = c.take<uint8_t>(Q.ovf_cap * Q.psz);
+        Q.w.ovf_cap = Q.ovf_cap;
+        Q.w.ovf_used = c.take<unsigned long long>(1);
+        Q.w.err = c.take<int>(1);
+        Q.d_scr = c.take<uint8_t>((size_t)Q.grid * Q.scr);
+    };
+    {
+        Carver probe(nullptr);
+        EncPass Q;
+        Q.wide = P.wide; Q.ovf_cap = P.ovf_cap; Q.psz = P.psz; Q.grid = P.grid; Q.scr = P.scr;
+        need(probe, Q);
+        // the split form's coder may still read its own allocations, never the arena; a
+        // reallocation still waits for it (the coder's records live apart, but not its caller)
+        if (probe.off + 4096 > ctx->arena_size && ctx->rc_pending) HIPCHK(hipEventSynchronize(ctx->rc_done));
+        if (!ctx->ensure_arena(probe.off + 4096)) return ctx->fail(LZMA_E_NOMEM, "device workspace %zu bytes", probe.off);
+    }
+    Carver c(ctx->arena);
+    need(c, P);
+    if (P.split) {
+        // records apart from the match finder's buffers; the coder's per-stream arrays apart
+        // from the pass arrays the next pass's staging rewrites
+        const size_t coder_bytes = (size_t)(ns + 1) * 8 * 4 + (size_t)ns * 8 + (size_t)ns * kRcSegs * kRcSegWords * 4 + 4096;
+        if ((rec_bytes_all > ctx->split_recs.n || coder_bytes > ctx->split_coder.n) && ctx->rc_pending)
+            HIPCHK(hipEventSynchronize(ctx->rc_done));
+        if (!ctx->split_recs.ensure(std::max<size_t>(rec_bytes_all, 256)) || !ctx->split_coder.ensure(coder_bytes))
+            return ctx->fail(LZMA_E_NOMEM, "coder records %zu bytes", rec_bytes_all);
+        P.d_recs = ctx->split_recs.as<uint16_t>();
+    }
+    return LZMA_OK;
+}
+
+// host arrays through pinned staging (see HostBuf): the pass's later host round trip
+// (the match finder's chain count) comes after these copies, so the staging is free
+// again when the next pass fills it
+static int pass_stage(Ctx* ctx, EncPass& P, hipStream_t st) {
+    const size_t pn = (size_t)P.ns + 1;
+    if (!ctx->pin.ensure(pn * 8 * 5 + pn * 4 * 2)) return ctx->fail(LZMA_E_NOMEM, "pinned staging");
+    uint64_t* p_offs = ctx->pin.as<uint64_t>();
+    uint64_t* p_oofs = p_offs + pn;
+    uint64_t* p_rofs = p_oofs + pn;
+    uint32_t* p_order = (uint32_t*)(p_rofs + pn + pn);
+    memcpy(p_offs, P.offs.data(), pn * 8);
+    memcpy(p_oofs, P.oofs.data(), pn * 8);
+    memcpy(p_rofs, P.rofs.data(), pn * 8);
+    memcpy(p_order, P.order.data(), (size_t)P.ns * 4);
+    TimedLaunch tl(ctx, "enc_stage", st);
+    HIPCHK(hipMemcpyAsync(P.inpad, P.d_in + P.in0, P.total, hipMemcpyDeviceToDevice, st));
+    HIPCHK(hipMemsetAsync(P.inpad + P.total, 0, 512, st));
+    HIPCHK(hipMemcpyAsync(P.d_offs, p_offs, pn * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(P.d_oofs, p_oofs, pn * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(P.d_order, p_order, P.ns * 4, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(P.d_rofs, p_rofs, pn * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemsetAsync(P.d_next, 0, 16, st));
+    return LZMA_OK;
+}
+
+// the walk; on a full overflow pool, grow it (4x, remembered by the context) and run the
+// pass's match finder again from the staging. Returns LZMA_OK or an error.
+static int pass_mf_back(Ctx* ctx, EncPass& P, hipStream_t st) {
+    for (int attempt = 0; attempt < 6; attempt++) {
+        int rc = mf_back(ctx, P.d, P.inpad, P.d_offs, P.ns, P.total, P.wide, P.w, st);
+        if (rc != LZMA_E_OVERFLOW) return rc;
+        if (P.slots_per_k >= 1024) return ctx->fail(LZMA_E_INTERNAL, "overflow pool full at one slot per position");
+        P.slots_per_k = std::min<uint64_t>(1024, P.slots_per_k * 4);
+        ctx->ovf_hint = P.slots_per_k;
+        P.ovf_cap = P.pool_cap(P.slots_per_k);
+        if ((rc = pass_carve(ctx, P)) || (rc = pass_stage(ctx, P, st)) ||
+            (rc = mf_front(ctx, P.d, P.inpad, P.d_offs, P.ns, P.total, P.wide, P.w, st)))
+            return rc;
+    }
+    return ctx->fail(LZMA_E_NOMEM, "match-pair overflow pool kept overflowing");
+}
+
+static int pass_parse(Ctx* ctx, EncPass& P, hipStream_t st) {
+    EncArgs a{};
+    a.in = P.inpad; a.offs = P.d_offs; a.order = P.d_order; a.nstreams = P.ns; a.next = P.d_next;
+    a.pairs = P.w.pairs; a.ovf_off = P.w.ovf_off; a.ovf = P.w.ovf;
+    a.recs = P.d_recs; a.rec_offs = P.d_rofs; a.rec_lens = P.d_rlens; a.out_lens = P.d_lens; a.status = P.d_status;
+    a.scratch = P.d_scr; a.scratch_stride = P.scr;
+    a.lit_stride = (enc_lit_bytes(P.d) + 255) & ~(size_t)255;
+    if (!ctx->ensure_litbuf((size_t)P.grid * a.lit_stride + 256)) return ctx->fail(LZMA_E_NOMEM, "literal-coder tables");
+    a.lit_scratch = ctx->litbuf;
+    const Derived& d = P.d;
+    a.fb = d.fb; a.lc = d.lc; a.lp = d.lp; a.pb = d.pb; a.eos = d.eos;
+    a.dist_table_size = d.dist_table_size; a.len_table_size = d.len_table_size;
+    a.lit_in_lds = enc_lit_in_lds(d, P.grid);
+    a.pair_bytes = P.wide ? 8 : 4;
+    LZG_TRACE(ctx, st, "encode pass: %d streams, %llu bytes, grid %d", P.ns, (unsigned long long)P.total, P.grid);
+    DebugWatch watch;
+    if (ctx->debug) { watch.start(16); a.dbg = watch.dev; }
+#ifdef LZG_PROF
+    uint64_t* d_prof = nullptr;
+    HIPCHK(hipMalloc(&d_prof, (size_t)P.ns * kProfSlots * 8));
+    HIPCHK(hipMemsetAsync(d_prof, 0, (size_t)P.ns * kProfSlots * 8, st));
+    a.prof = d_prof;
+#endif
+    // a pipelined caller's decoder (another context) may still hold CUs: the
+    // parser needs every stream resident from its start, so it waits for it
+    if (ctx->fence && ok_ctx(ctx->fence) && ctx->fence->dec_pending)
+        HIPCHK(hipStreamWaitEvent(st, ctx->fence->dec_done, 0));
+    int rc = launch_encoder(ctx, a, P.wide, P.grid, st);
+    if (rc) return rc;
+    LZG_TRACE(ctx, st, "enc_parse done");
+    watch.stop();
+#ifdef LZG_PROF
+    report_profile(d_prof, P.ns, P.total, st);
+    hipFree(d_prof);
+#endif
+    return LZMA_OK;
+}
+
+// the range coder over the parser's records (the coder's arrays: the pass's own, or the
+// split form's copies)
+static int pass_rc(Ctx* ctx, EncPass& P, uint64_t* rofs, uint64_t* rlens, uint32_t* order, int32_t* status, uint64_t* oofs,
+                   uint64_t* lens, uint32_t* seg, hipStream_t st) {
+    RcArgs ra{};
+    ra.recs = P.d_recs; ra.rec_offs = rofs; ra.rec_lens = rlens; ra.order = order; ra.nstreams = P.ns;
+    ra.status = status; ra.out = P.d_out; ra.out_offs = oofs; ra.out_lens = lens; ra.seg = seg;
+    int rc = launch_rc(ctx, ra, st);
+    LZG_TRACE(ctx, st, "enc_rc done");
+    return rc;
+}
+
+// one synchronous pass (dump != null: stop after the match finder and copy its output
+// to the host)
 static int encode_pass(Ctx* ctx, const Derived& d, const uint8_t* d_in, const uint64_t* h_offs, int s0, int s1,
                        uint8_t* d_out, const uint64_t* h_out_offs, uint64_t* h_out_lens, int32_t* h_status,
                        hipStream_t st, MatchDump* dump = nullptr) {
     if (ctx->dec_pending) return ctx->fail(LZMA_E_PARAM, "an asynchronous decode is in flight: lzma_dec_batch_dev_wait first");
-    const int ns = s1 - s0;
-    const uint64_t in0 = h_offs[s0];
-    const uint64_t total = h_offs[s1] - in0;
-    bool wide = false;
-    std::vector<uint64_t> offs(ns + 1), oofs(ns + 1);
-    for (int i = 0; i <= ns; i++) { offs[i] = h_offs[s0 + i] - in0; oofs[i] = h_out_offs[s0 + i]; }
-    for (int i = 0; i < ns; i++)
-        if (offs[i + 1] - offs[i] >= PairPack<uint32_t>::kMaxStream) wide = true;
-    const size_t psz = wide ? 8 : 4;
-    // longest streams first (work queue order)
-    std::vector<uint32_t> order(ns);
-    std::iota(order.begin(), order.end(), 0u);
-    std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
-        return (offs[a + 1] - offs[a]) > (offs[b + 1] - offs[b]);
-    });
-    const int grid = enc_grid(d, ns);
-    const size_t scr = (enc_scratch_per_block(d) + 255) & ~(size_t)255;
-    // overflow pool in slots of ovf_stride(fb) pairs, one slot per position with more
-    // than kInlinePairs pairs: start at 1 slot per 16 positions (a retry grows it 4x and
-    // remembers the rate for later passes of this context), never more than one per position
-    const uint64_t stride = ovf_stride(d.fb);
-    uint64_t slots_per_k = std::max<uint64_t>(64, ctx->ovf_hint);
-    auto pool_cap = [&](uint64_t spk) {
-        uint64_t slots = std::min<uint64_t>(total, (total * spk + 1023) / 1024) + 64;
-        return slots * stride;
-    };
-    uint64_t ovf_cap = pool_cap(slots_per_k);
-    // coder records (rc.hip) per stream: capacity layout in records, 64-record aligned
-    std::vector<uint64_t> rofs(ns + 1, 0);
-    for (int i = 0; i < ns; i++) rofs[i + 1] = rofs[i] + rc_record_bound(offs[i + 1] - offs[i]);
-    for (int attempt = 0; attempt < 6; attempt++) {
-        const uint64_t T = total;
-        // buffers only the match finder uses; the coder records reuse their memory after the walk
-        auto phase1 = [&](Carver& c, MfBuffers& w) {
-            w.k4 = c.take<uint64_t>(T); w.k3 = c.take<uint64_t>(T); w.k2 = c.take<uint64_t>(T); w.ks = c.take<uint64_t>(T);
-            w.vals = c.take<uint32_t>(T); w.vs = c.take<uint32_t>(T);
-            w.prev2 = c.take<uint32_t>(T); w.prev3 = c.take<uint32_t>(T);
-            w.flag = c.take<uint8_t>(T);
-            w.chain_start = c.take<uint32_t>(T); w.chain_len = c.take<uint32_t>(T); w.long_list = c.take<uint32_t>(T);
-            w.chain_idx = c.take<uint32_t>(T); w.chain_order = c.take<uint32_t>(T);
-            w.cls = c.take<uint32_t>(96);
-            w.son = c.take<uint64_t>(4 * T);   // mf.hip WNode: 32 bytes per position
-            w.hist = c.take<uint32_t>((size_t)ns * 1024);
-            w.seg_end = c.take<uint64_t>((size_t)ns + 1);
-            w.chain_offs = c.take<uint64_t>((size_t)ns + 1);
-        };
-        size_t p1_bytes;
-        {
-            MfBuffers pw{};
-            Carver probe(nullptr);
-            phase1(probe, pw);
-            p1_bytes = probe.off;
-        }
-        const size_t union_bytes = std::max<size_t>(p1_bytes, rofs[ns] * 2);
-        uint16_t* d_recs = nullptr;
-        uint64_t *d_rofs = nullptr, *d_rlens = nullptr;
-        uint32_t* d_seg = nullptr;
-        auto need = [&](Carver& c, MfBuffers& w, uint8_t** inpad, uint64_t** d_offs, uint64_t** d_oofs,
-                        uint32_t** d_order, uint64_t** d_lens, int32_t** d_status, unsigned** d_next, uint8_t** d_scr) {
-            *inpad = c.take<uint8_t>(T + 512);
-            *d_offs = c.take<uint64_t>(ns + 1);
-            *d_oofs = c.take<uint64_t>(ns + 1);
-            *d_order = c.take<uint32_t>(ns);
-            *d_lens = c.take<uint64_t>(ns);
-            *d_status = c.take<int32_t>(ns);
-            *d_next = c.take<unsigned>(4);
-            d_rofs = c.take<uint64_t>(ns + 1);
-            d_rlens = c.take<uint64_t>(ns);
-            d_seg = c.take<uint32_t>((size_t)ns * kRcSegs * kRcSegWords);
-            uint8_t* u = c.take<uint8_t>(union_bytes);
-            d_recs = (uint16_t*)u;
-            Carver c1(u);
-            phase1(c1, w);
-            w.pairs = (v4u32*)c.take<uint8_t>(T * rec_bytes(wide));
-            w.ovf_off = c.take<uint32_t>(T);
-            w.ovf = c.take<uint8_t>(ovf_cap * psz);
-            w.ovf_cap = ovf_cap;
-            w.ovf_used = c.take<unsigned long long>(1);
-            w.err = c.take<int>(1);
-            *d_scr = c.take<uint8_t>((size_t)grid * scr);
-        };
-        MfBuffers w{};
-        uint8_t *inpad, *d_scr;
-        uint64_t *d_offs, *d_oofs, *d_lens;
-        uint32_t* d_order;
-        int32_t* d_status;
-        unsigned* d_next;
-        {
-            Carver probe(nullptr);
-            need(probe, w, &inpad, &d_offs, &d_oofs, &d_order, &d_lens, &d_status, &d_next, &d_scr);
-            if (!ctx->ensure_arena(probe.off + 4096)) return ctx->fail(LZMA_E_NOMEM, "device workspace %zu bytes", probe.off);
-        }
-        Carver c(ctx->arena);
-        need(c, w, &inpad, &d_offs, &d_oofs, &d_order, &d_lens, &d_status, &d_next, &d_scr);
-        // host arrays go through pinned staging (see HostBuf): the pass syncs on its
-        // lengths at the end, so the staging is free again when the next pass starts
-        const size_t pn = (size_t)ns + 1;
-        if (!ctx->pin.ensure(pn * 8 * 5 + pn * 4 * 2)) return ctx->fail(LZMA_E_NOMEM, "pinned staging");
-        uint64_t* p_offs = ctx->pin.as<uint64_t>();
-        uint64_t* p_oofs = p_offs + pn;
-        uint64_t* p_rofs = p_oofs + pn;
-        uint64_t* p_lens = p_rofs + pn;
-        uint32_t* p_order = (uint32_t*)(p_lens + pn);
-        int32_t* p_status = (int32_t*)(p_order + pn);
-        memcpy(p_offs, offs.data(), pn * 8);
-        memcpy(p_oofs, oofs.data(), pn * 8);
-        memcpy(p_rofs, rofs.data(), pn * 8);
-        memcpy(p_order, order.data(), (size_t)ns * 4);
-        {
-            TimedLaunch tl(ctx, "enc_stage", st);
-            HIPCHK(hipMemcpyAsync(inpad, d_in + in0, total, hipMemcpyDeviceToDevice, st));
-            HIPCHK(hipMemsetAsync(inpad + total, 0, 512, st));
-            HIPCHK(hipMemcpyAsync(d_offs, p_offs, pn * 8, hipMemcpyHostToDevice, st));
-            HIPCHK(hipMemcpyAsync(d_oofs, p_oofs, pn * 8, hipMemcpyHostToDevice, st));
-            HIPCHK(hipMemcpyAsync(d_order, p_order, ns * 4, hipMemcpyHostToDevice, st));
-            HIPCHK(hipMemcpyAsync(d_rofs, p_rofs, pn * 8, hipMemcpyHostToDevice, st));
-            HIPCHK(hipMemsetAsync(d_next, 0, 16, st));
-        }
-        int rc = run_match_finder(ctx, d, inpad, d_offs, ns, total, wide, w, st);
-        if (rc == LZMA_E_OVERFLOW) {
-            if (slots_per_k >= 1024) return ctx->fail(LZMA_E_INTERNAL, "overflow pool full at one slot per position");
-            slots_per_k = std::min<uint64_t>(1024, slots_per_k * 4);
-            ctx->ovf_hint = slots_per_k;
-            ovf_cap = pool_cap(slots_per_k);
-            continue;
-        }
-        if (rc) return rc;
-        if (dump) {
-            dump->wide = wide;
-            dump->stride = (uint32_t)stride;
-            dump->ovf_off.resize(total);
-            dump->recs.resize(total * rec_bytes(wide));
-            HIPCHK(hipMemcpyAsync(p_lens, w.ovf_used, 8, hipMemcpyDeviceToHost, st));
-            HIPCHK(hipStreamSynchronize(st));
-            const unsigned long long used = p_lens[0];
-            dump->ovf.resize(std::min<uint64_t>(used * stride, ovf_cap) * psz);
-            if (total) {
-                HIPCHK(hipMemcpyAsync(dump->ovf_off.data(), w.ovf_off, total * 4, hipMemcpyDeviceToHost, st));
-                HIPCHK(hipMemcpyAsync(dump->recs.data(), w.pairs, dump->recs.size(), hipMemcpyDeviceToHost, st));
-            }
-            if (!dump->ovf.empty()) HIPCHK(hipMemcpyAsync(dump->ovf.data(), w.ovf, dump->ovf.size(), hipMemcpyDeviceToHost, st));
-            HIPCHK(hipStreamSynchronize(st));
-            return LZMA_OK;
-        }
-        EncArgs a{};
-        a.in = inpad; a.offs = d_offs; a.order = d_order; a.nstreams = ns; a.next = d_next;
-        a.pairs = w.pairs; a.ovf_off = w.ovf_off; a.ovf = w.ovf;
-        a.recs = d_recs; a.rec_offs = d_rofs; a.rec_lens = d_rlens; a.out_lens = d_lens; a.status = d_status;
-        a.scratch = d_scr; a.scratch_stride = scr;
-        a.lit_stride = (enc_lit_bytes(d) + 255) & ~(size_t)255;
-        if (!ctx->ensure_litbuf((size_t)grid * a.lit_stride + 256)) return ctx->fail(LZMA_E_NOMEM, "literal-coder tables");
-        a.lit_scratch = ctx->litbuf;
-        a.fb = d.fb; a.lc = d.lc; a.lp = d.lp; a.pb = d.pb; a.eos = d.eos;
-        a.dist_table_size = d.dist_table_size; a.len_table_size = d.len_table_size;
-        a.lit_in_lds = enc_lit_in_lds(d, grid);
-        a.pair_bytes = wide ? 8 : 4;
-        LZG_TRACE(ctx, st, "encode pass: %d streams, %llu bytes, grid %d", ns, (unsigned long long)total, grid);
-        DebugWatch watch;
-        if (ctx->debug) { watch.start(16); a.dbg = watch.dev; }
-#ifdef LZG_PROF
-        uint64_t* d_prof = nullptr;
-        HIPCHK(hipMalloc(&d_prof, (size_t)ns * kProfSlots * 8));
-        HIPCHK(hipMemsetAsync(d_prof, 0, (size_t)ns * kProfSlots * 8, st));
-        a.prof = d_prof;
-#endif
-        // a pipelined caller's decoder (another context) may still hold CUs: the
-        // parser needs every stream resident from its start, so it waits for it
-        if (ctx->fence && ok_ctx(ctx->fence) && ctx->fence->dec_pending)
-            HIPCHK(hipStreamWaitEvent(st, ctx->fence->dec_done, 0));
-        if ((rc = launch_encoder(ctx, a, wide, grid, st))) return rc;
-        LZG_TRACE(ctx, st, "enc_parse done");
-        watch.stop();
-        RcArgs ra{};
-        ra.recs = d_recs; ra.rec_offs = d_rofs; ra.rec_lens = d_rlens; ra.order = d_order; ra.nstreams = ns;
-        ra.status = d_status; ra.out = d_out; ra.out_offs = d_oofs; ra.out_lens = d_lens; ra.seg = d_seg;
-        if ((rc = launch_rc(ctx, ra, st))) return rc;
-        LZG_TRACE(ctx, st, "enc_rc done");
-#ifdef LZG_PROF
-        report_profile(d_prof, ns, total, st);
-        hipFree(d_prof);
-#endif
-        HIPCHK(hipMemcpyAsync(p_lens, d_lens, ns * 8, hipMemcpyDeviceToHost, st));
-        HIPCHK(hipMemcpyAsync(p_status, d_status, ns * 4, hipMemcpyDeviceToHost, st));
+    if (ctx->split_state || ctx->rc_pending)
+        return ctx->fail(LZMA_E_PARAM, "a split encode is in flight on this context: lzma_enc_parse_dev_async / _wait first");
+    EncPass P;
+    pass_plan(ctx, P, d, d_in, h_offs, s0, s1, d_out, h_out_offs, false);
+    int rc;
+    if ((rc = pass_carve(ctx, P)) || (rc = pass_stage(ctx, P, st)) ||
+        (rc = mf_front(ctx, P.d, P.inpad, P.d_offs, P.ns, P.total, P.wide, P.w, st)) || (rc = pass_mf_back(ctx, P, st)))
+        return rc;
+    const int ns = P.ns;
+    const size_t pn = (size_t)ns + 1;
+    uint64_t* p_lens = ctx->pin.as<uint64_t>() + 3 * pn;
+    int32_t* p_status = (int32_t*)((uint32_t*)(p_lens + pn) + pn);
+    if (dump) {
+        const uint64_t total = P.total;
+        dump->wide = P.wide;
+        dump->stride = (uint32_t)P.stride;
+        dump->ovf_off.resize(total);
+        dump->recs.resize(total * rec_bytes(P.wide));
+        HIPCHK(hipMemcpyAsync(p_lens, P.w.ovf_used, 8, hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
-        memcpy(h_out_lens + s0, p_lens, (size_t)ns * 8);
-        memcpy(h_status + s0, p_status, (size_t)ns * 4);
+        const unsigned long long used = p_lens[0];
+        dump->ovf.resize(std::min<uint64_t>(used * P.stride, P.ovf_cap) * P.psz);
+        if (total) {
+            HIPCHK(hipMemcpyAsync(dump->ovf_off.data(), P.w.ovf_off, total * 4, hipMemcpyDeviceToHost, st));
+            HIPCHK(hipMemcpyAsync(dump->recs.data(), P.w.pairs, dump->recs.size(), hipMemcpyDeviceToHost, st));
+        }
+        if (!dump->ovf.empty()) HIPCHK(hipMemcpyAsync(dump->ovf.data(), P.w.ovf, dump->ovf.size(), hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
         return LZMA_OK;
     }
-    return ctx->fail(LZMA_E_NOMEM, "match-pair overflow pool kept overflowing");
+    if ((rc = pass_parse(ctx, P, st)) ||
+        (rc = pass_rc(ctx, P, P.d_rofs, P.d_rlens, P.d_order, P.d_status, P.d_oofs, P.d_lens, P.d_seg, st)))
+        return rc;
+    HIPCHK(hipMemcpyAsync(p_lens, P.d_lens, ns * 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(p_status, P.d_status, ns * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    memcpy(h_out_lens + s0, p_lens, (size_t)ns * 8);
+    memcpy(h_status + s0, p_status, (size_t)ns * 4);
+    return LZMA_OK;
+}
+
+static int check_batch(Ctx* ctx, const uint64_t* h_offs, const uint64_t* h_out_offs, int nstreams) {
+    for (int i = 0; i < nstreams; i++) {
+        if (h_offs[i + 1] < h_offs[i] || h_out_offs[i + 1] < h_out_offs[i]) return ctx->fail(LZMA_E_PARAM, "offsets not monotone");
+        if (h_offs[i + 1] - h_offs[i] >= (1ull << 31)) return ctx->fail(LZMA_E_PARAM, "stream %d >= 2 GiB", i);
+    }
+    return LZMA_OK;
 }
 
 static int encode_batch_dev(Ctx* ctx, const lzma_params* p, const uint8_t* d_in, const uint64_t* h_offs, int nstreams,
@@ -308,10 +405,8 @@ static int encode_batch_dev(Ctx* ctx, const lzma_params* p, const uint8_t* d_in,
     if (derive(*p, d) != LZMA_OK) return ctx->fail(LZMA_E_PARAM, "invalid lzma_params");
     if (nstreams < 0) return ctx->fail(LZMA_E_PARAM, "nstreams < 0");
     if (nstreams == 0) return LZMA_OK;
-    for (int i = 0; i < nstreams; i++) {
-        if (h_offs[i + 1] < h_offs[i] || h_out_offs[i + 1] < h_out_offs[i]) return ctx->fail(LZMA_E_PARAM, "offsets not monotone");
-        if (h_offs[i + 1] - h_offs[i] >= (1ull << 31)) return ctx->fail(LZMA_E_PARAM, "stream %d >= 2 GiB", i);
-    }
+    int crc = check_batch(ctx, h_offs, h_out_offs, nstreams);
+    if (crc) return crc;
     std::vector<int32_t> status(nstreams, 0);
     int s0 = 0;
     // h_out_lens doubles as a diagnostic for LZMA_E_INTERNAL: (reason << 32) | position
@@ -331,6 +426,104 @@ static int encode_batch_dev(Ctx* ctx, const lzma_params* p, const uint8_t* d_in,
             return ctx->fail(status[i], status[i] == LZMA_E_OVERFLOW ? "stream %d: output capacity too small%.0llu"
                                                                      : "stream %d: encoder consistency check tripped (%llx)",
                              i, (unsigned long long)h_out_lens[i]);
+    return LZMA_OK;
+}
+
+// ---- the split encode (lzma_enc_stage_dev / lzma_enc_parse_dev_async / _wait)
+// The coder's per-stream arrays, copied out of the pass arrays in one launch once the
+// parser is done: the next pass's staging rewrites the pass arrays while the coder runs.
+struct CoderArrays {
+    uint64_t *rofs, *rlens, *oofs, *lens;
+    uint32_t *order, *seg;
+    int32_t* status;
+};
+static CoderArrays coder_arrays(Ctx* ctx, int ns) {
+    Carver c(ctx->split_coder.as<uint8_t>());
+    CoderArrays r;
+    r.rofs = c.take<uint64_t>(ns + 1); r.oofs = c.take<uint64_t>(ns + 1);
+    r.rlens = c.take<uint64_t>(ns); r.lens = c.take<uint64_t>(ns);
+    r.order = c.take<uint32_t>(ns); r.status = c.take<int32_t>(ns);
+    r.seg = c.take<uint32_t>((size_t)ns * kRcSegs * kRcSegWords);
+    return r;
+}
+__global__ void coder_arrays_kernel(int ns, const uint64_t* rofs, const uint64_t* rlens, const uint64_t* oofs, const uint64_t* lens,
+                                    const uint32_t* order, const int32_t* status, CoderArrays o) {
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i <= ns; i += gridDim.x * blockDim.x) {
+        o.rofs[i] = rofs[i];
+        o.oofs[i] = oofs[i];
+        if (i < ns) { o.rlens[i] = rlens[i]; o.lens[i] = lens[i]; o.order[i] = order[i]; o.status[i] = status[i]; }
+    }
+}
+
+static int enc_stage_dev(Ctx* ctx, const lzma_params* p, const uint8_t* d_in, const uint64_t* h_offs, int nstreams,
+                         uint8_t* d_out, const uint64_t* h_out_offs, hipStream_t st) {
+    if (ctx->dec_pending) return ctx->fail(LZMA_E_PARAM, "an asynchronous decode is in flight: lzma_dec_batch_dev_wait first");
+    if (ctx->split_state) return ctx->fail(LZMA_E_PARAM, "a batch is already staged: lzma_enc_parse_dev_async first");
+    Derived d;
+    if (derive(*p, d) != LZMA_OK) return ctx->fail(LZMA_E_PARAM, "invalid lzma_params");
+    if (nstreams <= 0) return ctx->fail(LZMA_E_PARAM, "the split form needs at least one stream");
+    int rc = check_batch(ctx, h_offs, h_out_offs, nstreams);
+    if (rc) return rc;
+    const uint64_t pass_cap = std::min<uint64_t>(ctx->batch_bytes, (1ull << 31) - 1);
+    if (nstreams > kMaxStreamsPerPass || (nstreams > 1 && h_offs[nstreams] - h_offs[0] > pass_cap))
+        return ctx->fail(LZMA_E_PARAM, "the split form takes one pass: at most %d streams and batch_bytes of input", kMaxStreamsPerPass);
+    if (!ctx->split_pass) ctx->split_pass = new (std::nothrow) EncPass;
+    if (!ctx->split_pass) return ctx->fail(LZMA_E_NOMEM, "split pass");
+    EncPass& P = *ctx->split_pass;
+    P = EncPass();
+    pass_plan(ctx, P, d, d_in, h_offs, 0, nstreams, d_out, h_out_offs, true);
+    if ((rc = pass_carve(ctx, P)) || (rc = pass_stage(ctx, P, st)) ||
+        (rc = mf_front(ctx, P.d, P.inpad, P.d_offs, P.ns, P.total, P.wide, P.w, st)))
+        return rc;
+    ctx->split_state = 1;
+    return LZMA_OK;
+}
+
+static int enc_parse_dev_async(Ctx* ctx, hipStream_t st) {
+    if (!ctx->split_state) return ctx->fail(LZMA_E_PARAM, "nothing staged: lzma_enc_stage_dev first");
+    if (ctx->rc_pending) return ctx->fail(LZMA_E_PARAM, "the previous batch's coder is in flight: lzma_enc_parse_dev_wait first");
+    EncPass& P = *ctx->split_pass;
+    ctx->split_state = 0;   // from here on the staged pass is consumed (or failed)
+    int rc;
+    if ((rc = pass_mf_back(ctx, P, st)) || (rc = pass_parse(ctx, P, st))) return rc;
+    if (!ctx->rc_stream && hipStreamCreateWithFlags(&ctx->rc_stream, hipStreamNonBlocking) != hipSuccess)
+        return ctx->fail(LZMA_E_DEVICE, "coder stream");
+    if (!ctx->parse_done && hipEventCreateWithFlags(&ctx->parse_done, hipEventDisableTiming) != hipSuccess)
+        return ctx->fail(LZMA_E_DEVICE, "parse event");
+    if (!ctx->rc_done && hipEventCreateWithFlags(&ctx->rc_done, hipEventDisableTiming) != hipSuccess)
+        return ctx->fail(LZMA_E_DEVICE, "coder event");
+    HIPCHK(hipEventRecord(ctx->parse_done, st));
+    HIPCHK(hipStreamWaitEvent(ctx->rc_stream, ctx->parse_done, 0));
+    const CoderArrays ca = coder_arrays(ctx, P.ns);
+    hipLaunchKernelGGL(coder_arrays_kernel, dim3((P.ns + 256) / 256), dim3(256), 0, ctx->rc_stream, P.ns, P.d_rofs, P.d_rlens,
+                       P.d_oofs, P.d_lens, P.d_order, P.d_status, ca);
+    HIPCHK(hipGetLastError());
+    if ((rc = pass_rc(ctx, P, ca.rofs, ca.rlens, ca.order, ca.status, ca.oofs, ca.lens, ca.seg, ctx->rc_stream))) return rc;
+    HIPCHK(hipEventRecord(ctx->rc_done, ctx->rc_stream));
+    ctx->rc_pending = P.ns;
+    return LZMA_OK;
+}
+
+static int enc_parse_dev_wait(Ctx* ctx, uint64_t* h_out_lens) {
+    if (!ctx->rc_pending) return ctx->fail(LZMA_E_PARAM, "no coder in flight: lzma_enc_parse_dev_async first");
+    const int ns = ctx->rc_pending;
+    ctx->rc_pending = 0;
+    // no device-to-host copy waits behind the coder (it would hold the copy engine): they
+    // are queued once it is done
+    HIPCHK(hipEventSynchronize(ctx->rc_done));
+    if (!ctx->pin_rc.ensure((size_t)ns * 12 + 16)) return ctx->fail(LZMA_E_NOMEM, "pinned staging");
+    uint64_t* p_lens = ctx->pin_rc.as<uint64_t>();
+    int32_t* p_status = (int32_t*)(p_lens + ns);
+    const CoderArrays ca = coder_arrays(ctx, ns);
+    HIPCHK(hipMemcpyAsync(p_lens, ca.lens, (size_t)ns * 8, hipMemcpyDeviceToHost, ctx->rc_stream));
+    HIPCHK(hipMemcpyAsync(p_status, ca.status, (size_t)ns * 4, hipMemcpyDeviceToHost, ctx->rc_stream));
+    HIPCHK(hipStreamSynchronize(ctx->rc_stream));
+    memcpy(h_out_lens, p_lens, (size_t)ns * 8);
+    for (int i = 0; i < ns; i++)
+        if (p_status[i] != LZMA_OK)
+            return ctx->fail(p_status[i], p_status[i] == LZMA_E_OVERFLOW ? "stream %d: output capacity too small%.0llu"
+                                                                         : "stream %d: encoder consistency check tripped (%llx)",
+                             i, (unsigned long long)p_lens[i]);
     return LZMA_OK;
 }
 
@@ -410,6 +603,8 @@ static int decode_batch_dev_async(Ctx* ctx, const uint8_t props[5], const uint8_
                                   int nstreams, const int64_t* h_out_sizes, uint8_t* d_out, const uint64_t* h_out_offs,
                                   hipStream_t st) {
     if (ctx->dec_pending) return ctx->fail(LZMA_E_PARAM, "an asynchronous decode is already in flight on this context");
+    if (ctx->split_state || ctx->rc_pending)   // the decode carves the arena the staged pass holds
+        return ctx->fail(LZMA_E_PARAM, "a split encode is in flight on this context: lzma_enc_parse_dev_async / _wait first");
     if (nstreams <= 0) return nstreams == 0 ? LZMA_OK : ctx->fail(LZMA_E_PARAM, "nstreams < 0");
     const size_t n = (size_t)nstreams;
     const size_t words = (n + 1) * 3 + n + (n + 1) / 2 * 2 + 2;   // in_offs, sizes, out_offs, lens, order + status
@@ -547,6 +742,15 @@ void lzma_ctx_destroy(lzma_ctx* ctx) {
     for (auto e : ctx->free_events) hipEventDestroy(e);
     if (ctx->dec_pending) hipEventSynchronize(ctx->dec_done);
     if (ctx->dec_done) hipEventDestroy(ctx->dec_done);
+    if (ctx->rc_pending) hipEventSynchronize(ctx->rc_done);
+    if (ctx->split_state) hipDeviceSynchronize();   // a staged pass's match finder may still run
+    if (ctx->rc_done) hipEventDestroy(ctx->rc_done);
+    if (ctx->parse_done) hipEventDestroy(ctx->parse_done);
+    if (ctx->rc_stream) hipStreamDestroy(ctx->rc_stream);
+    delete ctx->split_pass;
+    ctx->split_recs.release();
+    ctx->split_coder.release();
+    ctx->pin_rc.release();
     if (ctx->dec_host) hipHostFree(ctx->dec_host);
     if (ctx->arena) hipFree(ctx->arena);
     if (ctx->litbuf) hipFree(ctx->litbuf);
@@ -600,6 +804,28 @@ int lzma_enc_batch_dev(lzma_ctx* ctx, const lzma_params* p, const uint8_t* d_in,
     return encode_batch_dev(ctx, p, d_in, h_offs, nstreams, d_out, h_out_offs, h_out_lens, (hipStream_t)hip_stream);
 }
 
+int lzma_enc_stage_dev(lzma_ctx* ctx, const lzma_params* p, const uint8_t* d_in, const uint64_t* h_offs, int nstreams,
+                       uint8_t* d_out, const uint64_t* h_out_offs, void* hip_stream) {
+    if (!ok_ctx(ctx) || !p || !h_offs || !h_out_offs) return LZMA_E_PARAM;
+    if (check_device(ctx)) return LZMA_E_NODEVICE;
+    hipSetDevice(ctx->device);
+    return enc_stage_dev(ctx, p, d_in, h_offs, nstreams, d_out, h_out_offs, (hipStream_t)hip_stream);
+}
+
+int lzma_enc_parse_dev_async(lzma_ctx* ctx, void* hip_stream) {
+    if (!ok_ctx(ctx)) return LZMA_E_PARAM;
+    if (check_device(ctx)) return LZMA_E_NODEVICE;
+    hipSetDevice(ctx->device);
+    return enc_parse_dev_async(ctx, (hipStream_t)hip_stream);
+}
+
+int lzma_enc_parse_dev_wait(lzma_ctx* ctx, uint64_t* h_out_lens) {
+    if (!ok_ctx(ctx) || !h_out_lens) return LZMA_E_PARAM;
+    if (check_device(ctx)) return LZMA_E_NODEVICE;
+    hipSetDevice(ctx->device);
+    return enc_parse_dev_wait(ctx, h_out_lens);
+}
+
 int lzma_pack_dev(lzma_ctx* ctx, const uint8_t* d_src, const uint64_t* h_src_offs, const uint64_t* h_lens, int nstreams,
                   uint8_t* d_dst, const uint64_t* h_dst_offs, void* hip_stream) {
     if (!ok_ctx(ctx) || !h_src_offs || !h_lens || !h_dst_offs || nstreams < 0) return LZMA_E_PARAM;
@@ -608,6 +834,8 @@ int lzma_pack_dev(lzma_ctx* ctx, const uint8_t* d_src, const uint64_t* h_src_off
     // the pack carves the front of the arena, where a decode in flight keeps its offsets
     // and results (decode_enqueue), and may grow (reallocate) it
     if (ctx->dec_pending) return ctx->fail(LZMA_E_PARAM, "an asynchronous decode is in flight: lzma_dec_batch_dev_wait first");
+    if (ctx->split_state || ctx->rc_pending)
+        return ctx->fail(LZMA_E_PARAM, "a split encode is in flight on this context: lzma_enc_parse_dev_async / _wait first");
     hipSetDevice(ctx->device);
     hipStream_t st = (hipStream_t)hip_stream;
     for (int i = 0; i < nstreams; i++)

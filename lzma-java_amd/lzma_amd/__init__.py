@@ -45,6 +45,7 @@ EXPORTED_SYMBOLS = [
     "lzma_mctx_create", "lzma_mctx_destroy", "lzma_mctx_last_error", "lzma_mctx_devices",
     "lzma_enc_batch_multi", "lzma_dec_batch_multi", "lzma_mctx_set_batch_bytes", "lzma_mctx_set_timing",
     "lzma_visible_on_error", "lzma_dec_batch_dev_async", "lzma_dec_batch_dev_wait", "lzma_ctx_set_parse_fence",
+    "lzma_enc_stage_dev", "lzma_enc_parse_dev_async", "lzma_enc_parse_dev_wait",
 ]
 
 
@@ -108,6 +109,9 @@ def lib():
         L.lzma_dec_batch_dev_async.argtypes = [vp, vp, vp, vp, i32, vp, vp, vp, vp]
         L.lzma_dec_batch_dev_wait.argtypes = [vp, vp, vp]
         L.lzma_ctx_set_parse_fence.argtypes = [vp, vp]
+        L.lzma_enc_stage_dev.argtypes = [vp, P, vp, vp, i32, vp, vp, vp]
+        L.lzma_enc_parse_dev_async.argtypes = [vp, vp]
+        L.lzma_enc_parse_dev_wait.argtypes = [vp, vp]
         L.lzma_decode.argtypes = [vp, vp, vp, u64, ctypes.c_int64, vp, u64, ctypes.POINTER(u64)]
         L.lzma_bench_generate.argtypes = [vp, u64]
         L.lzma_bench_generate.restype = None
@@ -321,6 +325,33 @@ class Context:
         out_offs = np.ascontiguousarray(out_offs, dtype=np.uint64)
         self.check(lib().lzma_enc_batch_dev(self.h, ctypes.byref(p), _dptr(d_in), offs.ctypes.data, n, _dptr(d_out),
                                             out_offs.ctypes.data, lens.ctypes.data, ctypes.c_void_p(stream_ptr)))
+        return lens[:n]
+
+    # the same encode in three calls (lzma_enc_stage_dev / _parse_dev_async / _parse_dev_wait):
+    # the range coder of one batch runs on the context's coder stream while the next
+    # batch's match finder runs on the caller's stream
+    def encode_stage_dev(self, d_in, offs: np.ndarray, p: Params, d_out, out_offs: np.ndarray, stream_ptr: int = 0) -> None:
+        """Stage a batch and enqueue its match finder's front; returns without waiting."""
+        n = len(offs) - 1
+        offs = np.ascontiguousarray(offs, dtype=np.uint64)
+        out_offs = np.ascontiguousarray(out_offs, dtype=np.uint64)
+        self.check(lib().lzma_enc_stage_dev(self.h, ctypes.byref(p), _dptr(d_in), offs.ctypes.data, n, _dptr(d_out),
+                                            out_offs.ctypes.data, ctypes.c_void_p(stream_ptr)))
+        self._staged_n = n
+
+    def encode_parse_dev_async(self, stream_ptr: int = 0) -> None:
+        """The staged batch's walk and parser on the caller's stream, its range coder on the
+        context's coder stream; returns without waiting for them."""
+        self.check(lib().lzma_enc_parse_dev_async(self.h, ctypes.c_void_p(stream_ptr)))
+        self._coder_n = getattr(self, "_staged_n", 0)
+        self._staged_n = 0
+
+    def encode_parse_dev_wait(self) -> np.ndarray:
+        """Wait for the range coder; the encoded lengths."""
+        n = getattr(self, "_coder_n", 0)
+        lens = np.zeros(max(n, 1), dtype=np.uint64)
+        self.check(lib().lzma_enc_parse_dev_wait(self.h, lens.ctypes.data))
+        self._coder_n = 0
         return lens[:n]
 
     def pack_dev(self, d_src, src_offs: np.ndarray, lens: np.ndarray, d_dst, stream_ptr: int = 0) -> np.ndarray:

@@ -80,3 +80,74 @@ def test_async_decode_and_parse_fence_emulated():
     assert r["outs2"]
     assert r["again"] == 0
     assert r["fence_errs"] == [True]
+
+
+def _split_worker(q):
+    import lzma_amd
+    lzma_amd.LIB_PATH = SIMT_LIB   # "device" pointers are host pointers in the emulation
+    try:
+        data = lzma_amd.bench_generate(6 * 3000 - 555).tobytes()
+        streams = [data[i:i + 3000] for i in range(0, len(data), 3000)]
+        p = lzma_amd.make_params(dict_size=1 << 20, fb=32)
+        ctx = lzma_amd.Context(0)
+        ref = ctx.encode_batch(streams, p)   # the synchronous encode
+        src = np.frombuffer(data + b"\0" * 16, dtype=np.uint8).copy()
+        offs = np.zeros(len(streams) + 1, dtype=np.uint64)
+        offs[1:] = np.cumsum([len(s) for s in streams])
+        caps = np.zeros(len(streams) + 1, dtype=np.uint64)
+        caps[1:] = np.cumsum([lzma_amd.enc_bound(len(s)) for s in streams])
+        outs = [np.zeros(int(caps[-1]) + 1, dtype=np.uint8) for _ in range(2)]
+
+        def got(buf, lens):
+            return [buf[int(caps[i]):int(caps[i]) + int(lens[i])].tobytes() for i in range(len(streams))]
+
+        def refused(call):
+            try:
+                call()
+                return False
+            except lzma_amd.LzmaError as e:
+                return e.code == lzma_amd.LZMA_E_PARAM
+
+        r = {}
+        r["parse_before_stage"] = refused(lambda: ctx.encode_parse_dev_async())
+        r["wait_before_parse"] = refused(lambda: ctx.encode_parse_dev_wait())
+        # the pipelined order: stage A, parse A, stage B (A's coder in flight), wait A, parse B, wait B
+        ctx.encode_stage_dev(src.ctypes.data, offs, p, outs[0].ctypes.data, caps)
+        r["stage_twice"] = refused(lambda: ctx.encode_stage_dev(src.ctypes.data, offs, p, outs[0].ctypes.data, caps))
+        r["sync_while_staged"] = refused(lambda: ctx.encode_batch_dev(src.ctypes.data, offs, p, outs[1].ctypes.data, caps))
+        r["pack_while_staged"] = refused(lambda: ctx.pack_dev(outs[0].ctypes.data, caps, np.ones(len(streams), np.uint64),
+                                                              outs[1].ctypes.data))
+        ctx.encode_parse_dev_async()
+        ctx.encode_stage_dev(src.ctypes.data, offs, p, outs[1].ctypes.data, caps)
+        r["parse_while_coder_pending"] = refused(lambda: ctx.encode_parse_dev_async())
+        lens_a = ctx.encode_parse_dev_wait()
+        ctx.encode_parse_dev_async()
+        lens_b = ctx.encode_parse_dev_wait()
+        r["a_equal"] = got(outs[0], lens_a) == ref
+        r["b_equal"] = got(outs[1], lens_b) == ref
+        # the synchronous entry points work again once the coder is collected
+        r["sync_after"] = ctx.encode_batch(streams[:2], p) == ref[:2]
+        # one pass only: a batch above batch_bytes is refused
+        ctx.set_batch_bytes(4096)
+        r["two_passes"] = refused(lambda: ctx.encode_stage_dev(src.ctypes.data, offs, p, outs[0].ctypes.data, caps))
+        ctx.close()
+        q.put(r)
+    except BaseException as e:   # reported to the parent
+        q.put(dict(error=repr(e)))
+
+
+@pytest.mark.timeout(600)
+def test_split_encode_emulated():
+    """lzma_enc_stage_dev / lzma_enc_parse_dev_async / _wait (the pipelined bench's
+    encode): in the pipelined order (the next batch staged while the coder is in
+    flight) both batches' bytes equal the synchronous encode's, and every call out of
+    order, or another entry point while a batch is staged, returns LZMA_E_PARAM."""
+    subprocess.check_call(["make", "-s", "-j", "8", "-C", SIMT, "so"])
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    pr = ctx.Process(target=_split_worker, args=(q,))
+    pr.start()
+    r = q.get(timeout=500)
+    pr.join(timeout=60)
+    assert "error" not in r, r.get("error")
+    assert all(r.values()), r
