@@ -12,11 +12,12 @@
 //     goes (the nodes along one path are distinct, so the prefetched values
 //     stay exact for the rest of the walk);
 //   * the literal coders (0x300 << (lc + lp) probabilities) live in a
-//     per-stream HBM area, so the LDS per stream stays small (fixed models,
-//     input ring, output window: ~3.5 KiB) and 16 streams share a CU; a
-//     literal's whole coder tree (plus the 8 matched-mode nodes along the
-//     match byte) is fetched in one round trip, issued before the isMatch
-//     decision so it overlaps with it;
+//     per-stream HBM area, except (LITP, lc + lp <= 3) their plain 256-node trees,
+//     which take 4 KiB of LDS: a literal outside matched mode then touches no HBM,
+//     and the LDS per stream (fixed models, input ring, output window, plain trees:
+//     ~9 KiB) still lets 16 streams share a CU; a literal's whole coder tree (plus
+//     the 8 matched-mode nodes along the match byte) is fetched in one round trip,
+//     issued before the isMatch decision so it overlaps with it;
 //   * compressed input is staged through an LDS ring (kIbuf bytes, refilled
 //     by all lanes at once);
 //   * the most recent kWin output bytes live in an LDS window (OutWindow,
@@ -53,12 +54,15 @@ DFI uint32_t vget(const uint32_t (&v)[kVS], uint32_t j) {
 // FairPrio rows of the decoder's waves (lzma_common.h)
 __device__ uint32_t g_dec_sched[kSchedRows * kSchedCols];
 
-template <int PBS>
+constexpr uint32_t kDecLitpBits = 3;   // LITP: lc + lp <= 3 (at most 8 plain trees of 256 nodes in LDS)
+
+template <int PBS, bool LITP>
 struct Dec {
     using PL = ProbLayout<PBS>;
     uint32_t lane;
     uint16_t* probs;              // LDS: fixed models
     uint16_t* lit;                // HBM: literal coders of this stream
+    uint16_t* litp;               // LITP: LDS, the plain trees (nodes 0x000-0x0FF of each coder), 256 per coder
     uint8_t* ibuf;                // LDS [kIbuf]
     uint8_t* win;                 // LDS [kWin]
     uint32_t lc, lp, pb, ps_mask, dict_check;
@@ -276,6 +280,9 @@ struct Dec {
             if (i0 + lane < (uint32_t)PL::COUNT) probs[i0 + lane] = kBitModelTotal >> 1;
         for (uint32_t i0 = 0; i0 < nlit; i0 += 2 * kWave)   // u32 pairs (nlit is even)
             if (i0 + 2 * lane < nlit) *(uint32_t*)(lit + i0 + 2 * lane) = (kBitModelTotal >> 1) * 0x10001u;
+        if (LITP)
+            for (uint32_t i0 = 0; i0 < (256u << kDecLitpBits); i0 += 2 * kWave)
+                *(uint32_t*)(litp + i0 + 2 * lane) = (kBitModelTotal >> 1) * 0x10001u;
         LANE_FENCE();
         ipos = 0;
         ibase = 0;
@@ -300,10 +307,12 @@ struct Dec {
             // (nodes 0-255) and, in matched mode, the 8 nodes along the match byte
             const bool matched = !st_is_char(state);   // only right after a match / rep: copy() left mb
             const uint32_t mb = matched ? mb_next : 0u;
-            uint16_t* sub = lit + (size_t)(((now & ((1u << lp) - 1)) << lc) + (prev >> (8 - lc))) * 0x300;
+            const uint32_t cidx = ((now & ((1u << lp) - 1)) << lc) + (prev >> (8 - lc));
+            uint16_t* sub = lit + (size_t)cidx * 0x300;
+            uint16_t* plain = LITP ? litp + cidx * 256u : sub;   // the plain tree (nodes < 0x100)
             T256 tt;
             uint32_t mv[kVS];
-            fetch256(sub, tt);
+            fetch256(plain, tt);
 #pragma unroll
             for (int s = 0; s < kVS; s++) {
                 const uint32_t i = (uint32_t)(s * kWave) + lane;
@@ -325,7 +334,7 @@ struct Dec {
                     for (uint32_t i = 0; i < 8; i++) {
                         uint32_t np;
                         const uint32_t x = dbit(node256(tt, sym, (int)i), &np);
-                        sub[sym] = (uint16_t)np;
+                        plain[sym] = (uint16_t)np;
                         sym = (sym << 1) | x;
                     }
                 } else
@@ -339,7 +348,7 @@ struct Dec {
                         prob = node256(tt, sym, (int)i);
                     }
                     const uint32_t x = dbit(prob, &np);
-                    sub[idx] = (uint16_t)np;   // every lane, same address and value
+                    (same ? sub : plain)[idx] = (uint16_t)np;   // every lane, same address and value
                     if (same && x != mbit) same = false;
                     sym = (sym << 1) | x;
                 }
@@ -423,16 +432,18 @@ struct Dec {
 };
 
 // LDS of one stream: fixed models, input ring, output window (16-byte aligned regions)
-template <int PBS>
-constexpr size_t kDecLdsBytes = (((size_t)ProbLayout<PBS>::COUNT * 2 + 15) & ~(size_t)15) + kIbuf + kWin;
+// and (LITP) the plain literal trees
+template <int PBS, bool LITP>
+constexpr size_t kDecLdsBytes = (((size_t)ProbLayout<PBS>::COUNT * 2 + 15) & ~(size_t)15) + kIbuf + kWin +
+                                (LITP ? (size_t)(256u << kDecLitpBits) * 2 : 0);
 
-template <int PBS>
+template <int PBS, bool LITP>
 __global__ void __launch_bounds__(kWave) dec_kernel(DecArgs a) {
     // a static LDS array (the layout is fixed per PBS): its address is known when the kernel
     // is compiled, so LDS offsets fold into the ds instructions (a dynamic extern array's
     // base is a link-time constant that costs an s_add per address computation)
-    __shared__ __attribute__((aligned(16))) uint8_t smem[kDecLdsBytes<PBS>];
-    Dec<PBS> d;
+    __shared__ __attribute__((aligned(16))) uint8_t smem[kDecLdsBytes<PBS, LITP>];
+    Dec<PBS, LITP> d;
     d.lane = threadIdx.x;
     d.lc = a.lc; d.lp = a.lp; d.pb = a.pb; d.ps_mask = (1u << a.pb) - 1; d.dict_check = a.dict_check;
     size_t off = 0;
@@ -440,6 +451,7 @@ __global__ void __launch_bounds__(kWave) dec_kernel(DecArgs a) {
     d.probs = (uint16_t*)take((size_t)ProbLayout<PBS>::COUNT * 2);
     d.ibuf = take(kIbuf);
     d.win = take(kWin);
+    d.litp = LITP ? (uint16_t*)take((size_t)(256u << kDecLitpBits) * 2) : nullptr;
     d.lit = (uint16_t*)(a.scratch + (size_t)blockIdx.x * a.scratch_stride);
     // one workgroup per stream; per-stream values are wave-uniform (readfirstlane keeps them scalar)
     const int s = __builtin_amdgcn_readfirstlane((int)a.order[blockIdx.x]);
@@ -475,7 +487,8 @@ int dec_grid(uint32_t, uint32_t, uint32_t, int nstreams) { return nstreams; }   
 template <int PBS>
 static void launch_dec(const DecArgs& a, int grid, size_t lds, hipStream_t st) {
     (void)lds;   // static LDS (kDecLdsBytes)
-    hipLaunchKernelGGL((dec_kernel<PBS>), dim3(grid), dim3(kWave), 0, st, a);
+    if (a.lc + a.lp <= kDecLitpBits) hipLaunchKernelGGL((dec_kernel<PBS, true>), dim3(grid), dim3(kWave), 0, st, a);
+    else hipLaunchKernelGGL((dec_kernel<PBS, false>), dim3(grid), dim3(kWave), 0, st, a);
 }
 
 int launch_decoder(Ctx* ctx, const DecArgs& a, int grid, hipStream_t st) {
