@@ -499,7 +499,7 @@ def _profile_prefix(wl):
 
 
 def _profile(name, wl):
-    """A committed per-kernel summary from profiles/ (written by tools/profile_round.sh
+    """A committed per-kernel summary from profiles/ (written by tools/r04/prof.sh
     over this same workload), or None when absent or taken on another workload."""
     path = os.path.join(REPO, "profiles", _profile_prefix(wl) + name)
     if not os.path.exists(path):
