@@ -5,7 +5,7 @@
 #   issue.json        SQ_INSTS_* issue counters (one pass)
 # Every GPU step has its own time limit; the first failure ends the script.
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-O=$R/gpurun_out/r04
+O=${PROF_OUT:-$R/gpurun_out/r04}
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
 fail() { echo "$1 failed rc=$2"; exit $2; }
