@@ -31,6 +31,10 @@
 
 namespace lzg {
 
+#ifndef LZG_DEC_FLUSH_NT
+#define LZG_DEC_FLUSH_NT 1   // the window's flush to HBM as non-temporal stores (A/B: 0 = cached stores)
+#endif
+
 constexpr uint32_t kIbuf = 256;     // input staging ring
 constexpr uint32_t kWin = 1024;     // output window in LDS (power of two)
 constexpr uint32_t kFlush = 128;    // window -> HBM flush granule
@@ -98,7 +102,10 @@ struct Dec {
         LANE_FENCE();
         for (uint32_t k0 = flushed; k0 < upto; k0 += kWave) {   // uniform trip count
             const uint32_t k = k0 + lane;
-            if (k < upto) __builtin_nontemporal_store(win[k & (kWin - 1)], out + k);
+            if (k < upto) {
+                if (LZG_DEC_FLUSH_NT) __builtin_nontemporal_store(win[k & (kWin - 1)], out + k);
+                else out[k] = win[k & (kWin - 1)];   // cached: a far match reads its source back from L2 / MALL
+            }
         }
         flushed = upto;
         LANE_FENCE();

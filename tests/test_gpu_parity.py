@@ -233,6 +233,42 @@ def test_gpu_device_resident_api(ctx):
         dctx.close()
 
 
+def test_gpu_split_encode_pipelined_order():
+    """lzma_enc_stage_dev / lzma_enc_parse_dev_async / _wait on the GPU, in the pipelined
+    order (batch B staged, its match finder running, while batch A's range coder runs on
+    the context's coder stream): both batches' bytes equal the oracle's Encoder.Code, and
+    a second parse before the wait is refused."""
+    torch = pytest.importorskip("torch")
+    c = lzma_amd.Context(0)
+    try:
+        data = [lzma_amd.bench_generate(1 << 20), lzma_amd.text_generate(1 << 20)]
+        n = 8
+        offs = np.linspace(0, 1 << 20, n + 1).astype(np.uint64)
+        caps = [lzma_amd.enc_bound(int(offs[i + 1] - offs[i])) for i in range(n)]
+        oo = np.zeros(n + 1, dtype=np.uint64)
+        oo[1:] = np.cumsum(caps)
+        p = lzma_amd.make_params(dict_size=1 << 26, fb=32)
+        st = torch.cuda.current_stream().cuda_stream
+        d_in = [torch.from_numpy(x).cuda() for x in data]
+        d_out = [torch.empty(int(oo[-1]), dtype=torch.uint8, device="cuda") for _ in data]
+        c.encode_stage_dev(d_in[0], offs, p, d_out[0], oo, st)
+        c.encode_parse_dev_async(st)
+        c.encode_stage_dev(d_in[1], offs, p, d_out[1], oo, st)
+        with pytest.raises(lzma_amd.LzmaError):
+            c.encode_parse_dev_async(st)   # batch A's coder is still to be collected
+        lens_a = c.encode_parse_dev_wait()
+        c.encode_parse_dev_async(st)
+        lens_b = c.encode_parse_dev_wait()
+        torch.cuda.synchronize()
+        for x, buf, lens in zip(data, d_out, (lens_a, lens_b)):
+            h = buf.cpu().numpy()
+            refs = orc.encode_many([x[int(offs[i]):int(offs[i + 1])].tobytes() for i in range(n)], _oparams(p))
+            for i in range(n):
+                assert h[int(oo[i]):int(oo[i] + lens[i])].tobytes() == refs[i], i
+    finally:
+        c.close()
+
+
 # ---------------------------------------------------------------- match lists (SURVEY 7.1 instrumented mode)
 
 _MF_CASES = [
