@@ -12,10 +12,10 @@
 //     goes (the nodes along one path are distinct, so the prefetched values
 //     stay exact for the rest of the walk);
 //   * the literal coders (0x300 << (lc + lp) probabilities) live in a
-//     per-stream HBM area, except (LITP, lc + lp <= 3) their plain 256-node trees,
-//     which take 4 KiB of LDS: a literal outside matched mode then touches no HBM,
-//     and the LDS per stream (fixed models, input ring, output window, plain trees:
-//     ~9 KiB) still lets 16 streams share a CU; a literal's whole coder tree (plus
+//     per-stream HBM area, except (LITP: lc + lp <= 3 and at most 8 streams per CU)
+//     their plain 256-node trees, which take 4 KiB of LDS: a literal outside matched
+//     mode then touches no HBM (at 16 streams per CU the LDS is left to the match
+//     finder's sorts a pipelined caller runs beside the decode); a literal's whole coder tree (plus
 //     the 8 matched-mode nodes along the match byte) is fetched in one round trip,
 //     issued before the isMatch decision so it overlaps with it;
 //   * compressed input is staged through an LDS ring (kIbuf bytes, refilled
@@ -491,10 +491,17 @@ static size_t dec_lds_bytes(uint32_t pb) {
 
 int dec_grid(uint32_t, uint32_t, uint32_t, int nstreams) { return nstreams; }   // one workgroup per stream
 
+// The plain literal trees go to LDS only when at most 8 streams share a CU: at 16 per
+// CU their 4 KiB each leave too little LDS for the match finder's sorts (24.6 KiB per
+// block) that a pipelined caller runs beside the decode (measured: bench step 919 ->
+// 994 ms with the sorts 72 -> 162 ms, profiles/r04/bench_dec_litp_16_per_cu.json).
+constexpr int kDecLitpMaxStreams = 2048;
+
 template <int PBS>
 static void launch_dec(const DecArgs& a, int grid, size_t lds, hipStream_t st) {
     (void)lds;   // static LDS (kDecLdsBytes)
-    if (a.lc + a.lp <= kDecLitpBits) hipLaunchKernelGGL((dec_kernel<PBS, true>), dim3(grid), dim3(kWave), 0, st, a);
+    if (a.lc + a.lp <= kDecLitpBits && grid <= kDecLitpMaxStreams)
+        hipLaunchKernelGGL((dec_kernel<PBS, true>), dim3(grid), dim3(kWave), 0, st, a);
     else hipLaunchKernelGGL((dec_kernel<PBS, false>), dim3(grid), dim3(kWave), 0, st, a);
 }
 
