@@ -230,7 +230,14 @@ struct Enc {
     FairPrio prio;
     // ---- per-position gather (see gather()): p = current position, equality masks per side
     uint32_t gp;
-    uint64_t gm0, gm1, gm2, gm3, gmp0, gmp1;
+    // RING (fb <= 32): 32-bit masks, bit k = offset k (0 .. 31), enough for every length up
+    // to fb; one scalar register each instead of two (the kernel is at its SGPR limit).
+    // Otherwise 64-bit masks, bit k = offset k - 1 (-1 .. 62). Compares past the window
+    // continue with match_len either way.
+    using GM = typename std::conditional<RING, uint32_t, uint64_t>::type;
+    static constexpr int kMB = RING ? 32 : 64;   // mask bits
+    static constexpr int kMO = RING ? 0 : 1;     // the bit of offset 0
+    GM gm0, gm1, gm2, gm3, gmp0, gmp1;
     uint32_t g_prev, g_cur, g_mb;   // bytes at p - 1 and p, and at p - rep0 - 1 (the match byte), from the gather
 #ifdef LZG_PROF
     uint64_t prof[kProfSlots];
@@ -427,22 +434,25 @@ struct Enc {
             v0[it] = in_byte(q - d0); v1[it] = in_byte(q - d1); v2[it] = in_byte(q - d2); v3[it] = in_byte(q - d3);
             if (with_pairs) { w0[it] = in_byte(q - e0); w1[it] = in_byte(q - e1); }
         }
-        gm0 = gm1 = gm2 = gm3 = gmp0 = gmp1 = 0;
+        uint64_t m0 = 0, m1 = 0, m2 = 0, m3 = 0, mp0 = 0, mp1 = 0;   // bit k: offset k - 1
 #pragma unroll
         for (int it = 0; it < kGI; it++) {
             const int sh = it * kWave;
             const uint32_t k = (uint32_t)sh + lane;
-            gm0 |= (uint64_t)wballot(va[it] == v0[it]) << sh;
-            gm1 |= (uint64_t)wballot(va[it] == v1[it]) << sh;
-            gm2 |= (uint64_t)wballot(va[it] == v2[it]) << sh;
-            gm3 |= (uint64_t)wballot(va[it] == v3[it]) << sh;
+            m0 |= (uint64_t)wballot(va[it] == v0[it]) << sh;
+            m1 |= (uint64_t)wballot(va[it] == v1[it]) << sh;
+            m2 |= (uint64_t)wballot(va[it] == v2[it]) << sh;
+            m3 |= (uint64_t)wballot(va[it] == v3[it]) << sh;
             if (with_pairs) {
-                gmp0 |= (uint64_t)wballot(va[it] == w0[it]) << sh;
-                gmp1 |= (uint64_t)wballot(va[it] == w1[it]) << sh;
+                mp0 |= (uint64_t)wballot(va[it] == w0[it]) << sh;
+                mp1 |= (uint64_t)wballot(va[it] == w1[it]) << sh;
             }
             win[k] = (uint8_t)va[it];   // the cur side only: the other sides' bytes are read (rarely, by a
                                          // two-step candidate's literal) straight from the stream
         }
+        constexpr int drop = 1 - kMO;   // RING: offset -1's bit goes
+        gm0 = (GM)(m0 >> drop); gm1 = (GM)(m1 >> drop); gm2 = (GM)(m2 >> drop); gm3 = (GM)(m3 >> drop);
+        gmp0 = (GM)(mp0 >> drop); gmp1 = (GM)(mp1 >> drop);
         // the three bytes every position step reads, straight from the loaded registers
         // (offsets -1 and 0 are window entries 0 and 1): no LDS round trip on the chain
         g_prev = lane_value(va, 0);
@@ -463,23 +473,26 @@ struct Enc {
     }
     // InWindow.GetMatchLen(index = o - 1, dist, limit) from the side's mask; the
     // part of the compare beyond the window continues with match_len.
-    FI uint32_t glen(uint64_t m, uint32_t dist, int32_t o, int32_t limit) {
+    FI uint32_t glen(GM m, uint32_t dist, int32_t o, int32_t limit) {
         const int64_t rem = (int64_t)n - ((int64_t)gp + o);
         if (limit > rem) limit = (int32_t)rem;
         if (limit <= 0) return 0;
-        const int b = o + 1;                       // 0 <= b <= kGW
+        const int b = o + kMO;                     // 0 <= b
         uint32_t r;
-        if (b >= kGW) r = 0;
+        if (b >= kMB) r = 0;
         else {
-            const uint64_t x = ~m >> b;            // bits past the window shift in as 0 (= "equal")
-            const uint32_t lim_w = (uint32_t)(kGW - b);
-            r = x ? (uint32_t)__builtin_ctzll(x) : 64u;
+            const GM x = (GM)~m >> b;              // bits past the window shift in as 0 (= "equal")
+            const uint32_t lim_w = (uint32_t)(kMB - b);
+            r = x ? (uint32_t)(RING ? __builtin_ctz((uint32_t)x) : __builtin_ctzll((uint64_t)x)) : (uint32_t)kMB;
             if (r > lim_w) r = lim_w;
         }
         if (r >= (uint32_t)limit) return (uint32_t)limit;
-        if ((uint32_t)b + r < (uint32_t)kGW) return r;   // mismatch inside the window
+        if ((uint32_t)b + r < (uint32_t)kMB) return r;   // mismatch inside the window
         return r + match_len(o + (int32_t)r - 1, dist, limit - (int32_t)r);
     }
+    // the mask bits of offsets o and o + 1 both set (true past the window: no pre-check there)
+    static FI bool eq2(GM m, uint32_t o) { return o + 1 + kMO >= (uint32_t)kMB || ((m >> (o + kMO)) & 3u) == 3u; }
+    static FI bool eq1(GM m, uint32_t o) { return ((m >> (o + kMO)) & 1u) != 0; }   // o + kMO < kMB
 
     // ------------------------------------------------------------ coder records
     // The range coder (RangeEncoder.java:38-87) does not feed back into the
@@ -1020,11 +1033,11 @@ struct Enc {
         uint32_t num_avail = avail() + 1;
         if (num_avail < 2) { *back_res = -1; LANE_FENCE(); return 1; }
         if (num_avail > (uint32_t)kMatchMaxLen) num_avail = kMatchMaxLen;
-        // a rep whose first byte differs (mask bit 1 clear) has length 0: no glen
-        uint32_t rl0 = (gm0 & 2u) ? glen(gm0, rp0, 0, kMatchMaxLen) : 0u;
-        uint32_t rl1 = (gm1 & 2u) ? glen(gm1, rp1, 0, kMatchMaxLen) : 0u;
-        uint32_t rl2 = (gm2 & 2u) ? glen(gm2, rp2, 0, kMatchMaxLen) : 0u;
-        uint32_t rl3 = (gm3 & 2u) ? glen(gm3, rp3, 0, kMatchMaxLen) : 0u;
+        // a rep whose first byte differs (offset 0's mask bit clear) has length 0: no glen
+        uint32_t rl0 = eq1(gm0, 0) ? glen(gm0, rp0, 0, kMatchMaxLen) : 0u;
+        uint32_t rl1 = eq1(gm1, 0) ? glen(gm1, rp1, 0, kMatchMaxLen) : 0u;
+        uint32_t rl2 = eq1(gm2, 0) ? glen(gm2, rp2, 0, kMatchMaxLen) : 0u;
+        uint32_t rl3 = eq1(gm3, 0) ? glen(gm3, rp3, 0, kMatchMaxLen) : 0u;
         PEND(PF_REPLEN, t0);
         uint32_t rep_max = 0, rl_max = rl0;
         if (rl1 > rl_max) { rep_max = 1; rl_max = rl1; }
@@ -1247,8 +1260,8 @@ struct Enc {
         uint32_t num_avail = num_avail_full;
         if (num_avail < 2) return;
         if (num_avail > fb) num_avail = fb;
-        // literal + rep0: lenTest2 >= 2 needs the bytes at offsets 1 and 2 equal (mask bits 2, 3)
-        if (!next_is_char && match_byte != cur_byte && (gm0 & 0xCu) == 0xCu) {
+        // literal + rep0: lenTest2 >= 2 needs the bytes at offsets 1 and 2 equal
+        if (!next_is_char && match_byte != cur_byte && eq2(gm0, 1)) {
             uint32_t t = num_avail_full - 1 < fb ? num_avail_full - 1 : fb;
             PBEGIN(t2a);
             uint32_t lt2 = glen(gm0, rp0, 1, (int32_t)t);
@@ -1268,9 +1281,9 @@ struct Enc {
 #pragma unroll
         for (uint32_t ri = 0; ri < (uint32_t)kNumRepDistances; ri++) {
             uint32_t rdist = sel4(ri, rp0, rp1, rp2, rp3);
-            const uint64_t gmr = ri == 0 ? gm0 : (ri == 1 ? gm1 : (ri == 2 ? gm2 : gm3));
-            // lenTest >= 2 needs offsets 0 and 1 equal (mask bits 1, 2): most reps stop here
-            if ((gmr & 6u) != 6u) continue;
+            const GM gmr = ri == 0 ? gm0 : (ri == 1 ? gm1 : (ri == 2 ? gm2 : gm3));
+            // lenTest >= 2 needs offsets 0 and 1 equal: most reps stop here
+            if (!eq2(gmr, 0)) continue;
             PBEGIN(tr);
             uint32_t lt = glen(gmr, rdist, 0, (int32_t)num_avail);
             PEND(PF_REPLEN, tr);
@@ -1280,8 +1293,8 @@ struct Enc {
             relax_rep(cur, 2, lt, rep_match_price + pure_rep_price(ri, st, pos_state), pos_state, cur, ri);
             PEND(PF_RELAX, trr);
             if (ri == 0) start_len = lt + 1;
-            // the two-step lenTest2 >= 2 needs offsets lt + 1 and lt + 2 equal (mask bits lt + 2, lt + 3)
-            if (lt < num_avail_full && (lt + 3 >= 64u || ((gmr >> (lt + 2)) & 3u) == 3u)) {
+            // the two-step lenTest2 >= 2 needs offsets lt + 1 and lt + 2 equal
+            if (lt < num_avail_full && eq2(gmr, lt + 1)) {
                 uint32_t t = num_avail_full - 1 - lt;
                 if (t > fb) t = fb;
                 PBEGIN(tq);
@@ -1336,8 +1349,8 @@ struct Enc {
                 PEND(PF_RELAX, tm);
                 uint32_t lt = seg_hi;
                 const int side = offs < 2 ? 5 + (int)offs : -1;
-                const uint64_t gmp = offs == 0 ? gmp0 : gmp1;
-                if (lt < num_avail_full && (side < 0 || lt + 3 >= 64u || ((gmp >> (lt + 2)) & 3u) == 3u)) {
+                const GM gmp = offs == 0 ? gmp0 : gmp1;
+                if (lt < num_avail_full && (side < 0 || eq2(gmp, lt + 1))) {
                     uint32_t t = num_avail_full - 1 - lt;
                     if (t > fb) t = fb;
                     PBEGIN(tm2);
@@ -1517,7 +1530,7 @@ struct Enc {
             md_buf = (PairT*)(lds_base + P->mdbuf_off);
             win = lds_base + P->win_off;
             rp0 = P->rp0; rp1 = P->rp1; rp2 = P->rp2; rp3 = P->rp3;
-            gm0 = P->gm0; gm1 = P->gm1; gm2 = P->gm2; gm3 = P->gm3; gmp0 = P->gmp0; gmp1 = P->gmp1;
+            gm0 = (GM)P->gm0; gm1 = (GM)P->gm1; gm2 = (GM)P->gm2; gm3 = (GM)P->gm3; gmp0 = (GM)P->gmp0; gmp1 = (GM)P->gmp1;
             uint32_t len_end = P->len_end;
             ring_top = P->ring_top; far_valid = P->far_valid; bad = 0;
             relax_step(cur, position, r, next_is_char, match_price, rep_match_price, new_len, npairs, len_end);
