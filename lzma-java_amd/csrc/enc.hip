@@ -1840,7 +1840,7 @@ size_t enc_scratch_per_block(const Derived&) { return (size_t)kNumOpts * 4 * 10 
 size_t enc_lit_bytes(const Derived& d) { return ((size_t)0x300 << (d.lc + d.lp)) * 2 + 2; }   // + the sink entry
 
 uint32_t enc_lit_in_lds(const Derived& d, int nstreams) {
-    static const int force = getenv("LZG_ENC_LITLDS") ? atoi(getenv("LZG_ENC_LITLDS")) : -1;   // A/B runs
+    static const int force = exp_env("LZG_ENC_LITLDS") ? atoi(exp_env("LZG_ENC_LITLDS")) : -1;   // A/B runs
     const uint32_t bits = d.lc + d.lp;
     if (bits <= (uint32_t)kLitLdsMaxBits) return 1;
     if (force >= 0) return force != 0 && bits <= (uint32_t)kLitLdsMaxBitsFew;
@@ -1890,7 +1890,7 @@ static void launch_pb(Ctx* ctx, const EncArgs& a, int grid, size_t lds, hipStrea
 // LZG_ENC_W2=1 (the CPU emulation test runs both forms).
 static bool want_w2(const EncArgs& a, int grid) {
     if (a.fb > 32) return false;   // the ring (SPEC 1 / 2) only
-    static const int force = getenv("LZG_ENC_W2") ? atoi(getenv("LZG_ENC_W2")) : -1;
+    static const int force = exp_env("LZG_ENC_W2") ? atoi(exp_env("LZG_ENC_W2")) : -1;
     return force > 0 && grid <= kFewStreams;
 }
 

@@ -604,7 +604,7 @@ static MfArgs mf_args(const Derived& d, const MfBuffers& w, uint64_t total, int 
     a.cut_value = d.cut_value; a.cyc_size = d.cyc_size; a.direct_bytes = d.direct_bytes;
     a.walk_lo = 0; a.walk_hi = 0xFFFFFFFFu;
     a.total = total; a.nstreams = nstreams;
-    if (const char* e = getenv("LZG_WALK_ONLY")) {   // "lo,hi": a timing experiment; the output is incomplete
+    if (const char* e = exp_env("LZG_WALK_ONLY")) {   // "lo,hi": a timing experiment; the output is incomplete
         unsigned lo = 0, hi = 0xFFFFFFFFu;
         if (sscanf(e, "%u,%u", &lo, &hi) >= 1) { a.walk_lo = lo; a.walk_hi = hi; }
     }
@@ -619,7 +619,7 @@ static MfArgs mf_args(const Derived& d, const MfBuffers& w, uint64_t total, int 
 // The long chains' scratch list: k4, dead since the hash4 sort (mf_chains_kernel fills it)
 static uint32_t mf_long_min() {
     // LZG_WALK_LONG overrides the long-chain threshold (experiments; 4294967295 = stream order only)
-    static const uint32_t long_min = getenv("LZG_WALK_LONG") ? (uint32_t)strtoul(getenv("LZG_WALK_LONG"), nullptr, 10) : kWalkLong;
+    static const uint32_t long_min = exp_env("LZG_WALK_LONG") ? (uint32_t)strtoul(exp_env("LZG_WALK_LONG"), nullptr, 10) : kWalkLong;
     return long_min;
 }
 
@@ -711,7 +711,7 @@ int mf_back(Ctx* ctx, const Derived& d, const uint8_t* in, const uint64_t* d_off
         unsigned grid = (unsigned)((nchains + WB - 1) / WB);
         grid = ((grid + 7) & ~7u) + long_blocks;   // multiples of 8 (XCD-aware mapping in mf_walk_kernel)
         // experiment: dynamic LDS per wave caps the waves per CU (L2 working set)
-        static const size_t walk_lds = getenv("LZG_WALK_LDS") ? (size_t)atoi(getenv("LZG_WALK_LDS")) : 0;
+        static const size_t walk_lds = exp_env("LZG_WALK_LDS") ? (size_t)atoi(exp_env("LZG_WALK_LDS")) : 0;
         if (wide_pairs) {
             if (bt4) hipLaunchKernelGGL((mf_walk_kernel<uint64_t, true>), dim3(grid), dim3(WB), walk_lds, st, in, d_offs, w.ks, w.vs, w.chain_order, w.chain_start, w.chain_len, nchains, w.long_list, (uint64_t)n_long, long_blocks, long_min, a, (WNode*)w.son, w.pairs, w.ovf_off, (uint64_t*)w.ovf, w.ovf_used, w.ovf_cap, ovf_stride(d.fb), w.err);
             else hipLaunchKernelGGL((mf_walk_kernel<uint64_t, false>), dim3(grid), dim3(WB), walk_lds, st, in, d_offs, w.ks, w.vs, w.chain_order, w.chain_start, w.chain_len, nchains, w.long_list, (uint64_t)n_long, long_blocks, long_min, a, (WNode*)w.son, w.pairs, w.ovf_off, (uint64_t*)w.ovf, w.ovf_used, w.ovf_cap, ovf_stride(d.fb), w.err);

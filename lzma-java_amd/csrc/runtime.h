@@ -21,6 +21,19 @@
 
 namespace lzg {
 
+// Experiment switches (A/B timing runs: walk subsets, thresholds, off-by-default kernel
+// variants) read the environment only in the experiment build (`make exp`, -DLZG_EXPERIMENT).
+// The product library ignores them, so its output never depends on the caller's environment.
+static inline const char* exp_env(const char* name) {
+#ifdef LZG_EXPERIMENT
+    return getenv(name);
+#else
+    (void)name;
+    return nullptr;
+#endif
+}
+
+
 struct MfArgs {
     uint32_t fb, min_match_check, hash_mask, hash_bits, cut_value, direct_bytes;
     uint32_t rec_vecs;            // 16-byte vectors per match-list record

@@ -318,9 +318,14 @@ static int pass_parse(Ctx* ctx, EncPass& P, hipStream_t st) {
     a.prof = d_prof;
 #endif
     // a pipelined caller's decoder (another context) may still hold CUs: the
-    // parser needs every stream resident from its start, so it waits for it
-    if (ctx->fence && ok_ctx(ctx->fence) && ctx->fence->dec_pending)
-        HIPCHK(hipStreamWaitEvent(st, ctx->fence->dec_done, 0));
+    // parser needs every stream resident from its start, so it waits for it. The
+    // fence is read under the live-context lock: lzma_ctx_destroy on another thread
+    // clears it (and destroys the event) only under that lock.
+    if (ctx->fence) {
+        std::lock_guard<std::mutex> g(g_ctx_lock);
+        const Ctx* f = ctx->fence;
+        if (f && g_live_ctx.count(const_cast<Ctx*>(f)) && f->dec_pending) HIPCHK(hipStreamWaitEvent(st, f->dec_done, 0));
+    }
     int rc = launch_encoder(ctx, a, P.wide, P.grid, st);
     if (rc) return rc;
     LZG_TRACE(ctx, st, "enc_parse done");
@@ -492,12 +497,16 @@ static int enc_parse_dev_async(Ctx* ctx, hipStream_t st) {
         return ctx->fail(LZMA_E_DEVICE, "parse event");
     if (!ctx->rc_done && hipEventCreateWithFlags(&ctx->rc_done, hipEventDisableTiming) != hipSuccess)
         return ctx->fail(LZMA_E_DEVICE, "coder event");
-    HIPCHK(hipEventRecord(ctx->parse_done, st));
-    HIPCHK(hipStreamWaitEvent(ctx->rc_stream, ctx->parse_done, 0));
+    // The copy of the pass arrays runs on the caller's stream, ahead of parse_done: a
+    // later lzma_enc_stage_dev on that stream rewrites the pass arrays (a new batch's
+    // offsets, order, status), and stream order keeps that behind this copy. Only the
+    // coder itself runs on the coder stream.
     const CoderArrays ca = coder_arrays(ctx, P.ns);
-    hipLaunchKernelGGL(coder_arrays_kernel, dim3((P.ns + 256) / 256), dim3(256), 0, ctx->rc_stream, P.ns, P.d_rofs, P.d_rlens,
+    hipLaunchKernelGGL(coder_arrays_kernel, dim3((P.ns + 256) / 256), dim3(256), 0, st, P.ns, P.d_rofs, P.d_rlens,
                        P.d_oofs, P.d_lens, P.d_order, P.d_status, ca);
     HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(ctx->parse_done, st));
+    HIPCHK(hipStreamWaitEvent(ctx->rc_stream, ctx->parse_done, 0));
     if ((rc = pass_rc(ctx, P, ca.rofs, ca.rlens, ca.order, ca.status, ca.oofs, ca.lens, ca.seg, ctx->rc_stream))) return rc;
     HIPCHK(hipEventRecord(ctx->rc_done, ctx->rc_stream));
     ctx->rc_pending = P.ns;

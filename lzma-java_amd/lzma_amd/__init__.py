@@ -600,6 +600,10 @@ class Decoder:
                 cap *= 4
                 continue
             break
+        if st not in (LZMA_OK, LZMA_E_DATA):
+            # not a verdict on the data (the reference throws, as the JNI shim does): no
+            # unvalidated output reaches the caller's stream
+            raise LzmaError(st, "Decoder.Code: status %d" % st)
         if st == LZMA_E_DATA:
             # Code returns false with only the whole windows OutWindow flushed so far
             # written (OutWindow.java:63-73; window = max(dict, 4096), Decoder.java:167)

@@ -39,7 +39,14 @@
 #define kBitModelTotal 2048            /* RangeBase.java:5 */
 #define kNumMoveBits 5                 /* RangeBase.java:7 */
 #define kTopMask 0xFF000000u           /* RangeBase.java:6 */
-#define kMaxValForNormalize ((1u << 30) - 1) /* BinTree.java:19 */
+/* BinTree.java:19. A test build lowers it (ORACLE_MAX_VAL_FOR_NORMALIZE, oracle/Makefile
+ * `norm`) so that Normalize runs on streams of a few MiB: tests/test_oracle.py pins that it
+ * changes no output bit, the premise of the GPU match finder's 1-based
+ * absolute positions. */
+#ifndef ORACLE_MAX_VAL_FOR_NORMALIZE
+#define ORACLE_MAX_VAL_FOR_NORMALIZE ((1u << 30) - 1)
+#endif
+#define kMaxValForNormalize (ORACLE_MAX_VAL_FOR_NORMALIZE)
 
 /* ------------------------------------------------------------------ tables */
 static uint32_t g_crc[256];        /* CRC.java:11-25 */
@@ -249,7 +256,10 @@ static int bt_create(bt_t *t, const uint8_t *buf, uint64_t n, uint32_t dict, uin
 }
 static void bt_free(bt_t *t) { free(t->son); free(t->hash); t->son = t->hash = NULL; t->son_cap = t->hash_cap = 0; }
 
+static uint64_t g_normalize_calls;           /* how often Normalize ran (tests) */
+uint64_t oracle_normalize_count(void) { return g_normalize_calls; }
 static void bt_normalize(bt_t *t) {          /* BinTree.java:358-375 */
+    g_normalize_calls++;
     uint32_t sub = t->pos - t->cyc_size;
     for (uint64_t i = 0; i < (uint64_t)t->cyc_size * 2; i++) { uint32_t v = t->son[i]; t->son[i] = v <= sub ? 0 : v - sub; }
     for (uint32_t i = 0; i < t->hash_size_sum; i++) { uint32_t v = t->hash[i]; t->hash[i] = v <= sub ? 0 : v - sub; }

@@ -72,6 +72,8 @@ int oracle_rc_encode_bits(const int32_t *bits, int n, uint8_t *out, int cap);
 int oracle_rc_direct_bits(const uint32_t *vals, const int32_t *nbits, int n, uint8_t *out, int cap);
 void oracle_bittree_prices_after(int num_bit_levels, int encoded_symbol, uint32_t *prices);
 uint32_t oracle_prob_price(int index);
+/* Normalize calls so far (BinTree.java:358-375; the `norm` test build lowers its threshold) */
+uint64_t oracle_normalize_count(void);
 
 #ifdef __cplusplus
 }

@@ -269,6 +269,104 @@ def test_gpu_split_encode_pipelined_order():
         c.close()
 
 
+def test_gpu_split_encode_heterogeneous_batches():
+    """The split encode with batches of DIFFERENT layouts: batch B has more
+    streams, ragged sizes and a larger total than batch A, and is staged -- its offsets,
+    order and status rewritten into the pass arrays, its match finder enqueued -- while
+    batch A's range coder may still run on the coder stream. Both batches byte-equal to the
+    oracle's Encoder.Code. Guards the copy of the coder's per-stream arrays, which must be
+    ordered before the next stage's rewrites (runtime.hip enc_parse_dev_async)."""
+    torch = pytest.importorskip("torch")
+    c = lzma_amd.Context(0)
+    try:
+        p = lzma_amd.make_params(dict_size=1 << 26, fb=32)
+        st = torch.cuda.current_stream().cuda_stream
+        rng = np.random.default_rng(55)
+        batches = []
+        for size, n in ((1 << 20, 8), (3 << 20, 13)):
+            x = lzma_amd.bench_generate(size) if n == 8 else lzma_amd.text_generate(size)
+            cuts = np.sort(rng.integers(1, size, n - 1)) if n != 8 else np.linspace(0, size, n + 1)[1:-1]
+            offs = np.concatenate([[0], cuts, [size]]).astype(np.uint64)
+            caps = [lzma_amd.enc_bound(int(offs[i + 1] - offs[i])) for i in range(n)]
+            oo = np.zeros(n + 1, dtype=np.uint64)
+            oo[1:] = np.cumsum(caps)
+            batches.append((x, offs, oo, torch.from_numpy(x).cuda(),
+                            torch.empty(int(oo[-1]), dtype=torch.uint8, device="cuda")))
+        (xa, oa, ooa, ia, da), (xb, ob, oob, ib, db) = batches
+        c.encode_stage_dev(ia, oa, p, da, ooa, st)
+        c.encode_parse_dev_async(st)
+        c.encode_stage_dev(ib, ob, p, db, oob, st)   # B's layout rewrites the pass arrays
+        lens_a = c.encode_parse_dev_wait()
+        c.encode_parse_dev_async(st)
+        lens_b = c.encode_parse_dev_wait()
+        torch.cuda.synchronize()
+        for x, offs, oo, buf, lens in ((xa, oa, ooa, da, lens_a), (xb, ob, oob, db, lens_b)):
+            n = len(offs) - 1
+            h = buf.cpu().numpy()
+            refs = orc.encode_many([x[int(offs[i]):int(offs[i + 1])].tobytes() for i in range(n)], _oparams(p))
+            for i in range(n):
+                assert h[int(oo[i]):int(oo[i] + lens[i])].tobytes() == refs[i], (n, i)
+    finally:
+        c.close()
+
+
+def test_gpu_encode_beside_decode_two_hip_streams():
+    """An encode on one context and HIP stream while a batch decode runs on another context
+    and HIP stream, with no parse fence: the two kernels' waves share the CUs. Regression
+    test for round 3's fault (mf_chains_kernel's two block scans shared LDS words; waves
+    that drifted apart beside decoder waves corrupted the chain lists, mf.hip): every
+    stream of the concurrent encode equals the sequential encode, a spread sample equals
+    the oracle's Encoder.Code, and the decode round-trips."""
+    import threading
+    torch = pytest.importorskip("torch")
+    dev = torch.device("cuda", 0)
+    chunk, n = 256 << 10, 1024
+    host = lzma_amd.bench_generate(n * chunk)
+    offs = np.arange(n + 1, dtype=np.uint64) * np.uint64(chunk)
+    cap_offs = np.zeros(n + 1, dtype=np.uint64)
+    cap_offs[1:] = np.cumsum([lzma_amd.enc_bound(chunk)] * n)
+    d_in = torch.from_numpy(host).to(dev)
+    d_comp = torch.empty(int(cap_offs[-1]), dtype=torch.uint8, device=dev)
+    d_comp2 = torch.empty_like(d_comp)
+    d_pack = torch.empty_like(d_comp)
+    d_pack2 = torch.empty_like(d_comp)
+    d_dec = torch.zeros(n * chunk, dtype=torch.uint8, device=dev)
+    p = lzma_amd.make_params(dict_size=1 << 26, fb=32)
+    props = lzma_amd.write_props(p)
+    sizes = np.full(n, chunk, dtype=np.int64)
+    sa, sb = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    ce, cd = lzma_amd.Context(0), lzma_amd.Context(0)
+    try:
+        ce.set_batch_bytes(1 << 30)
+        lens = ce.encode_batch_dev(d_in, offs, p, d_comp, cap_offs, sa.cuda_stream)
+        pk = ce.pack_dev(d_comp, cap_offs, lens, d_pack, sa.cuda_stream)
+        torch.cuda.synchronize()
+        for rep in range(2):   # two rounds: the decode overlaps the match finder and the parse
+            d_dec.zero_()
+            torch.cuda.synchronize()
+            cd.decode_batch_dev_async(props, d_pack, pk, sizes, d_dec, offs, sb.cuda_stream)
+            got = {}
+            th = threading.Thread(target=lambda: got.update(r=cd.decode_batch_dev_wait()))
+            th.start()
+            lens2 = ce.encode_batch_dev(d_in, offs, p, d_comp2, cap_offs, sa.cuda_stream)
+            th.join()
+            torch.cuda.synchronize()
+            dl, ds = got["r"]
+            assert (ds == 0).all() and (dl == chunk).all() and torch.equal(d_dec, d_in)
+            assert np.array_equal(lens, lens2)
+            pk2 = ce.pack_dev(d_comp2, cap_offs, lens2, d_pack2, sa.cuda_stream)
+            torch.cuda.synchronize()
+            assert np.array_equal(pk, pk2) and torch.equal(d_pack[:int(pk[-1])], d_pack2[:int(pk2[-1])])
+        idx = np.linspace(0, n - 1, 24).astype(int)
+        hp = d_pack2[:int(pk2[-1])].cpu().numpy()
+        ref = orc.encode_many([host[int(offs[i]):int(offs[i + 1])].tobytes() for i in idx], _oparams(p))
+        for i, r in zip(idx, ref):
+            assert hp[int(pk2[i]):int(pk2[i + 1])].tobytes() == r, i
+    finally:
+        ce.close()
+        cd.close()
+
+
 # ---------------------------------------------------------------- match lists (SURVEY 7.1 instrumented mode)
 
 _MF_CASES = [

@@ -160,3 +160,49 @@ def test_decoder_rejects_corrupt_distance():
         rc, _ = orc.decode(junk, bytes([0x5D, 0, 0, 0, 1]), 1000)
         bad += rc == 0
     assert bad > 0
+
+
+def _norm_lib():
+    """The oracle built with Normalize at 2^20 - 1 instead of 2^30 - 1 (oracle/Makefile `norm`)."""
+    import ctypes
+    import subprocess
+    so = os.path.join(orc.ORACLE_DIR, "build", "norm", "liblzma_oracle.so")
+    src = os.path.join(orc.ORACLE_DIR, "lzma_oracle.c")
+    if not os.path.exists(so) or os.path.getmtime(so) < os.path.getmtime(src):
+        subprocess.check_call(["make", "-s", "-C", orc.ORACLE_DIR, "norm"])
+    L = ctypes.CDLL(so)
+    u8p = ctypes.POINTER(ctypes.c_uint8)
+    L.oracle_encode.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(orc.Params), ctypes.c_int,
+                                ctypes.POINTER(u8p), ctypes.POINTER(ctypes.c_uint64)]
+    L.oracle_free.argtypes = [ctypes.c_void_p]
+    L.oracle_normalize_count.restype = ctypes.c_uint64
+    return L
+
+
+@pytest.mark.parametrize("kind,kw", [("bench", dict(dict_size=1 << 16, fb=32, mf=1)),
+                                     ("text", dict(dict_size=1 << 18, fb=32, mf=1)),
+                                     ("bench", dict(dict_size=1 << 16, fb=64, mf=0))],
+                         ids=["bench-bt4-d16", "text-bt4-d18", "bench-bt2-d16"])
+def test_normalize_is_output_neutral(kind, kw):
+    """VERDICT r04 (config 4's regime): BinTree.Normalize (BinTree.java:358-375) runs when
+    _pos reaches kMaxValForNormalize (:19, 88-90), i.e. once per ~1 GiB in the reference.
+    The GPU match finder never renormalises (absolute positions, streams < 2^31), which is
+    bit-exact only if Normalize changes no output bit. Pinned here with the
+    oracle rebuilt to normalise at 2^20 - 1: 4 MiB streams then normalise several times and
+    must give exactly the bytes of the normal build, which never normalises below 2^30."""
+    import ctypes
+    import lzma_amd
+    data = (lzma_amd.bench_generate if kind == "bench" else lzma_amd.text_generate)(4 << 20).tobytes()
+    p = orc.params(**kw)
+    L = _norm_lib()
+    before = L.oracle_normalize_count()
+    a, ptr = orc._buf(data)
+    out = ctypes.POINTER(ctypes.c_uint8)()
+    n = ctypes.c_uint64()
+    assert L.oracle_encode(ptr, a.size, ctypes.byref(p), 0, ctypes.byref(out), ctypes.byref(n)) == 0
+    got = ctypes.string_at(out, n.value)
+    L.oracle_free(out)
+    runs = L.oracle_normalize_count() - before
+    # Normalize at every (2^20 - 1) - cyclicBufferSize positions: (4 MiB) / (~2^20 - dict)
+    assert runs >= (4 << 20) // (1 << 20)
+    assert got == orc.encode(data, p)
