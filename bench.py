@@ -161,6 +161,9 @@ class Device:
         if not self.emulate:
             torch.cuda.synchronize(self.dev)
 
+    def cus(self):
+        return 256 if self.emulate else torch.cuda.get_device_properties(self.dev).multi_processor_count
+
     def new_stream(self):
         # the encoder and decoder run on HIP streams of their own: work on the null stream
         # would wait for every other stream's work
@@ -209,7 +212,12 @@ def run_pass(args, D, p, ctxs, strong, rank, world, dist):
     props = lzma_amd.write_props(p)
     D.sync()   # the input copy above ran on the current stream
     state = {"dec_ok": True}
-    if overlap:   # the parse of step k+1 waits for step k's decode
+    # The parse of step k+1 waits for step k's decode when the streams fill the CUs (the
+    # parser wants every stream resident from its start: 16 per CU at 4096). At <= 8 streams
+    # per CU (strong-scaling shares) the parse and decode waves fit beside each other, so the
+    # parse starts at once and step k's decode runs beside it.
+    fence = overlap and n > 8 * D.cus()
+    if fence:
         ctx.set_parse_fence(ctx_dec)
 
     def check_dec(dlens, dstat):
@@ -224,7 +232,7 @@ def run_pass(args, D, p, ctxs, strong, rank, world, dist):
             check_dec(*ctx_dec.decode_batch_dev(props, buf, pk, out_sizes, d_dec, offs, st_dec))
         state["t_dec"] = state.get("t_dec", 0.0) + (time.perf_counter() - t1)
 
-    def join():   # the previous step's decode (with --overlap; done by now: this step's parse waited for it)
+    def join():   # the previous step's decode (pipelined: with the fence, done by now)
         if state.pop("dec_inflight", False):
             check_dec(*ctx_dec.decode_batch_dev_wait())
 
@@ -278,8 +286,9 @@ def run_pass(args, D, p, ctxs, strong, rank, world, dist):
     join()
     barrier()
     elapsed = time.perf_counter() - t0
-    if overlap:
+    if fence:
         ctx.set_parse_fence(None)
+    if overlap:
         # the phases overlap: their MB/s come from the summed kernel times (HIP events)
         state["t_dec"] = sum(v[0] for k_, v in ctx_dec.timings().items()) / 1e3
         state["t_enc"] = sum(v[0] for k_, v in ctx.timings().items()) / 1e3
@@ -324,7 +333,22 @@ def run_pass(args, D, p, ctxs, strong, rank, world, dist):
             if strong and args.dump_container:
                 with open(args.dump_container, "wb") as f:
                     f.write(blob)
+    # one buffer encoded, packed and decoded back to back (no pipelining): what a single
+    # step costs on its own, reported beside the pipelined steady-state value
+    barrier()
+    t1 = time.perf_counter()
+    lens1 = ctx.encode_batch_dev(d_in, offs, p, d_comp, cap_offs, st)
+    pk1 = ctx.pack_dev(d_comp, cap_offs, lens1, d_packs[0], st)
+    dl1, ds1 = ctx_dec.decode_batch_dev(props, d_packs[0], pk1, out_sizes, d_dec, offs, st_dec)
+    barrier()
+    seq_elapsed = time.perf_counter() - t1
+    seq_ok = bool((ds1 == 0).all()) and bool((dl1 == out_sizes).all()) and bool(np.array_equal(lens1, state["lens"]))
+    if dist:
+        t = torch.tensor([seq_elapsed], dtype=torch.float64, device=D.dev)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        seq_elapsed = float(t.item())
     return {"elapsed": elapsed, "timings": timings, "state": state, "host": host, "full": full, "offs": offs,
+            "seq_elapsed": seq_elapsed, "seq_ok": seq_ok, "fence": fence,
             "n": n, "n_all": n_all, "size": size, "my_size": my_size, "comp_bytes": comp_bytes,
             "roundtrip": roundtrip, "t_enc": state["t_enc"], "t_dec": state["t_dec"], "gathered": gathered,
             "bufs": (d_in, d_comp, d_packs, d_dec)}
@@ -467,6 +491,11 @@ def main():
                          "phase's summed kernel times (HIP events), which overlap" % (
                              args.pipeline, "range coder (the encoder's coder stream), pack and "
                              if args.pipeline == "split" else "")),
+            "sequential": {"value": size / r["seq_elapsed"] / 1e6, "unit": "MB/s", "ms": r["seq_elapsed"] * 1e3,
+                           "lengths_equal_timed_steps": r["seq_ok"],
+                           "note": "one buffer encoded, packed and decoded back to back after the timed loop (no "
+                                   "pipelining): the cost of one step on its own; value is the pipelined steady state"},
+            "parse_fence": r["fence"],
             "ratio": ratio, "chunking": chunking, "verified": ok,
             "verified_means": "every stream decodes to its input and every sampled stream's bytes equal the "
                               "oracle's Encoder.Code restatement%s" % (

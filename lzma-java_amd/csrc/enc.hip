@@ -54,8 +54,27 @@ constexpr int kTpBytes = 2 * kNumFullDistances;   // tempPrices (u16 [kNumFullDi
 static_assert(kTpBytes >= kGW, "the gather window holds the cur side");
 constexpr int kRbuf = 128;          // coder-record staging ring (records, power of two; halves of 64 go to HBM)
 constexpr int kLitSlots = (8 + kWave - 1) / kWave;   // literal bits per lane (1 on hardware)
+// _optimum's pp word: PosPrev (bits 0-11), PosPrev2 (12-23; slots < kNumOpts = 4096) and the
+// flags Prev1IsChar | Prev2 << 1 (24-25). A candidate that clears Prev1IsChar writes the whole
+// word (PosPrev2 and Prev2 are read only with Prev1IsChar set): no read-modify-write.
+constexpr uint32_t kPosMask = 0xFFFu, kPos2Shift = 12, kFlagShift = 24;
+static_assert(kNumOpts <= 4096, "PosPrev fits 12 bits");
 
 #define FI __device__ __forceinline__
+// Parse-kernel variants under A/B measurement (0 = off in the product build; `make exp` style
+// builds set them with -D): see DESIGN.md section 5, round 5.
+#ifndef LZG_EXP_BRANCHFREE_STATE
+#define LZG_EXP_BRANCHFREE_STATE 0
+#endif
+#ifndef LZG_EXP_PARK
+#define LZG_EXP_PARK 0
+#endif
+#ifndef LZG_EXP_LITPF
+#define LZG_EXP_LITPF 0
+#endif
+#ifndef LZG_EXP_STATIC_LDS
+#define LZG_EXP_STATIC_LDS 1   // measured: one stream -9 %, 512 streams -10 %, 4096 flat (round 5)
+#endif
 // Lanes of one wavefront exchange data through LDS. The hardware runs one
 // wave's LDS instructions in order; this compiler barrier keeps the IR and
 // machine schedulers from moving LDS accesses across an exchange point.
@@ -66,7 +85,6 @@ constexpr int kLitSlots = (8 + kWave - 1) / kWave;   // literal bits per lane (1
 // bookkeeping on every iteration and makes values after it look per-lane).
 #define LANE_FOR(T, v, lo, hi) \
     for (T v##_0 = (lo); v##_0 < (hi); v##_0 += kWave) if (const T v = v##_0 + (T)lane; v < (hi))
-// every loop spends from one per-stream budget; exhausting it records the loop id
 // debug checkpoint (block 0, lane 0) into host-mapped memory
 // (LZG_DEBUG builds only)
 #ifdef LZG_DEBUG
@@ -74,9 +92,8 @@ constexpr int kLitSlots = (8 + kWave - 1) / kWave;   // literal bits per lane (1
 #else
 #define DBG(k, v) do {} while (0)
 #endif
-// The two unbounded-looking loops (the per-call parse loop and the per-symbol
-// coding loop) spend from one budget; the inner loops are bounded by design.
-#define WDOG(id) if (++wd > wd_max) { bad = 100 + (id); break; }
+// Every loop is bounded: the forward loop by kNumOpts (cur < kNumOpts - 1 is checked), the
+// coding loop by the stream length (every symbol advances now_pos by >= 1 or the stream ends).
 // Phase profile (profiling build only, -DLZG_PROF): s_memtime cycles per phase,
 // summed per stream into EncArgs::prof[stream * kProfSlots + phase].
 #ifdef LZG_PROF
@@ -91,8 +108,7 @@ constexpr int kLitSlots = (8 + kWave - 1) / kWave;   // literal bits per lane (1
 #endif
 
 // A ballot over this wave's lanes. The CPU emulation (LZG_WAVE = 1) runs each wave as
-// one lane: its own bit, with no collective across the block (the two-wave kernel's
-// waves run different code, and the emulation's collectives are block-wide).
+// one lane: its own bit.
 FI uint64_t wballot(bool p) {
 #if LZG_WAVE == 1
     return p ? 1ull : 0ull;
@@ -100,6 +116,8 @@ FI uint64_t wballot(bool p) {
     return __ballot(p);
 #endif
 }
+
+FI uint32_t uni32(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
 
 FI uint64_t uni64(uint64_t v) {
     return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32)) << 32) |
@@ -137,30 +155,8 @@ FI uint32_t sel4(uint32_t i, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
 // FairPrio rows of the encoder's waves (lzma_common.h)
 __device__ uint32_t g_enc_sched[kSchedRows * kSchedCols];
 
-// The two-wave parse (W2, few streams per CU): wave 0 (A) runs the serial chain, wave 1
-// (B) the candidate relaxations of a forward position (R) beside A's state / gather /
-// literal-price work for the next one (S). Each round is two workgroup barriers: P (B has
-// finished R(c); A has finished S(c + 1)) and Q (A has updated slot c + 1's literal /
-// short-rep candidates and handed R(c + 1) over). Everything B needs crosses in this LDS
-// record, which A writes only between P and Q (B reads it right after Q); slot contents
-// are shared through the _optimum ring itself.
-enum : uint32_t { kPipeIdle = 0, kPipeRelax = 1, kPipeExit = 2 };
-struct Pipe {
-    uint32_t ctrl;
-    uint32_t cur, position, st, pos_state, cur_and1, cur_byte, match_byte;
-    uint32_t next_is_char, match_price, rep_match_price, new_len, npairs;
-    uint32_t gp, mfpos, md_off, mdbuf_off, win_off;
-    uint32_t rp0, rp1, rp2, rp3;
-    uint32_t len_end, ring_top, far_valid, bad;   // the pass's shared state: B's during R, A's otherwise
-    uint32_t pad;
-    uint64_t gm0, gm1, gm2, gm3, gmp0, gmp1;
-};
-
-template <typename PairT, bool LIT_LDS, int PBS, bool RING, bool W2 = false>
+template <typename PairT, bool LIT_LDS, int PBS, bool RING>
 struct Enc {
-    // W2: a 64-entry match-list ring filled 32 entries at a time (A's fill for c + 1 keeps
-    // c's entry, which B still reads), and md_buf / the gather window double-buffered
-    static constexpr uint32_t kRingN = W2 ? 2 * (uint32_t)kRing : (uint32_t)kRing;
     using PP = PairPack<PairT>;
     using PL = ProbLayout<PBS>;
     static constexpr int E_IS_MATCH = PL::IS_MATCH, E_IS_REP = PL::IS_REP, E_G0 = PL::G0, E_G1 = PL::G1,
@@ -182,19 +178,14 @@ struct Enc {
     uint16_t* tp;             // tempPrices [128]
     const PairT* mdp;         // the current position's pairs (packed): its ring slot, or md_buf
     PairT* md_buf;            // a copy when the list is longer than the inline pairs or is clamped
-    PairT* md_buf_alt;        // W2: the other position's md_buf
     uint8_t* win;             // gather window: the cur side's bytes at offsets -1 .. kGW - 2 (aliased by tp)
-    uint8_t* win_alt;         // W2: the other position's gather window
-    uint8_t* lds_base;        // W2: LDS offsets in the hand-off
-    Pipe* pipe;               // W2: the hand-off record
     uint32_t* ring_info;      // [kRing]
     PairT* ring_pairs;        // [kRing * kInlinePairs]
     uint32_t* o_price;        // _optimum SoA, [kOptLds] each (+ the sink entry, + kFarEntry)
     uint32_t* o_pp;
     int32_t* o_bp;
     int32_t* o_bp2;
-    uint8_t* o_fs;
-    uint32_t* o_backs;        // [4][kOptLds]
+    uint32_t* o_backs;        // [kOptLds][4] (one 16-byte record per slot: Backs0..3)
     uint32_t* o_bytes;        // [kOptLds] cur byte | match byte << 8 | previous byte << 16 of each parsed
                               // position, so the coder needs no HBM byte loads (RING: | state << 24)
     uint16_t* rbuf;           // coder-record staging ring [kRbuf]
@@ -206,7 +197,6 @@ struct Enc {
     __amdgpu_buffer_rsrc_t inb;   // the stream's bytes, range-checked (out of range reads 0, never fault)
     uint32_t n;
     uint32_t bad;                 // internal-consistency watchdog tripped (reason code, 0 = fine)
-    uint32_t wd, wd_max;          // loop-iteration watchdog (budget per stream)
     uint32_t* dbg;
     uint16_t* recs;           // the stream's coder records in HBM (rc.hip codes them)
     uint64_t rcap, rpos;      // record capacity / records emitted
@@ -227,7 +217,15 @@ struct Enc {
     // ---- RING bookkeeping of _optimum (see the accessors)
     uint32_t ring_top;        // highest slot whose ahead fields are in the ring
     uint32_t far_valid;       // slot cur + 65 is held in the far entry (kFarEntry)
-    FairPrio prio;
+    // The coder's state, parked in LDS while getOptimum's forward loop runs (park / unpark):
+    // none of it is read there, so none of it holds a register there (the kernel is at its
+    // SGPR limit). FairPrio's state lives only here.
+    struct Cold {
+        uint64_t recs, rcap, rpos;
+        uint32_t rd0, rd1, rd2, rd3, state, prev_byte, mpc, apc, overflow, dts;
+        FairPrio prio;
+    };
+    Cold* cold;
     // ---- per-position gather (see gather()): p = current position, equality masks per side
     uint32_t gp;
     // RING (fb <= 32): 32-bit masks, bit k = offset k (0 .. 31), enough for every length up
@@ -239,6 +237,14 @@ struct Enc {
     static constexpr int kMO = RING ? 0 : 1;     // the bit of offset 0
     GM gm0, gm1, gm2, gm3, gmp0, gmp1;
     uint32_t g_prev, g_cur, g_mb;   // bytes at p - 1 and p, and at p - rep0 - 1 (the match byte), from the gather
+    uint32_t g_next;                // byte at p + 1 (the next position's literal), from the gather
+#if LZG_EXP_LITPF
+    // The next forward position's literal probabilities, loaded one position ahead (its coder
+    // and symbol are input bytes, known before its state is): bit slot j's three candidates
+    // (normal, matched with match bit 0, matched with match bit 1). The literal coders do not
+    // change within a forward pass (only the coder, between passes, adapts them).
+    uint32_t lpf0[kLitSlots], lpf1[kLitSlots], lpf2[kLitSlots];
+#endif
 #ifdef LZG_PROF
     uint64_t prof[kProfSlots];
 #endif
@@ -276,17 +282,30 @@ struct Enc {
     template <bool F = false> FI void set_bp(uint32_t i, int32_t v) { if (F || a_in(i)) o_bp[ix(i)] = v; else sstore(2, i, (uint32_t)v); }
     template <bool F = false> FI int32_t bp2_at(uint32_t i) const { if (F || a_in(i)) return o_bp2[ix(i)]; return (int32_t)sload(3, i); }
     template <bool F = false> FI void set_bp2(uint32_t i, int32_t v) { if (F || a_in(i)) o_bp2[ix(i)] = v; else sstore(3, i, (uint32_t)v); }
-    template <bool F = false> FI uint32_t fs_at(uint32_t i) const { if (F || a_in(i)) return (uint32_t)o_fs[ix(i)]; return sload(4, i); }
-    template <bool F = false> FI void set_fs(uint32_t i, uint32_t v) { if (F || a_in(i)) o_fs[ix(i)] = (uint8_t)v; else sstore(4, i, v); }
+    // the flags (Prev1IsChar = bit 0, Prev2 = bit 1, Optimal.java:8-9) ride in pp's top byte
+    template <bool F = false> FI uint32_t fs_at(uint32_t i) const { return pp_at<F>(i) >> kFlagShift; }
     // behind fields: in RING mode a home read waits for the write-backs (rare: a
     // path back by 65 slots, or a coded literal 64 slots behind the parse end)
     template <bool F = false> FI uint32_t back_at(uint32_t i, int k, uint32_t top) const {
-        if (F || b_in(i, top)) return o_backs[k * kOptLds + ix(i)];
+        if (F || b_in(i, top)) return o_backs[ix(i) * 4 + k];
         if (RING) SPILL_FENCE();
         return sload(5 + k, i);
     }
     template <bool F = false> FI void set_back(uint32_t i, int k, uint32_t v) {
-        if (F || RING || i < (uint32_t)kOptLds) o_backs[k * kOptLds + ix(i)] = v; else sstore(5 + k, i, v);
+        if (F || RING || i < (uint32_t)kOptLds) o_backs[ix(i) * 4 + k] = v; else sstore(5 + k, i, v);
+    }
+    // all four Backs of slot i: one 16-byte LDS access (or the HBM home, as back_at)
+    template <bool F = false> FI v4u32 backs4_at(uint32_t i, uint32_t top) const {
+        if (F || b_in(i, top)) return *(const v4u32*)(o_backs + ix(i) * 4);
+        if (RING) SPILL_FENCE();
+        const v4u32 v = {sload(5, i), sload(6, i), sload(7, i), sload(8, i)};
+        return v;
+    }
+    template <bool F = false> FI void set_backs4(uint32_t i, uint32_t b0, uint32_t b1, uint32_t b2, uint32_t b3) {
+        if (F || RING || i < (uint32_t)kOptLds) {
+            const v4u32 v = {b0, b1, b2, b3};
+            *(v4u32*)(o_backs + ix(i) * 4) = v;
+        } else { sstore(5, i, b0); sstore(6, i, b1); sstore(7, i, b2); sstore(8, i, b3); }
     }
     template <bool F = false> FI uint32_t bytes_at(uint32_t i, uint32_t top) const {
         if (F || b_in(i, top)) return o_bytes[ix(i)];
@@ -297,26 +316,26 @@ struct Enc {
         if (F || RING || i < (uint32_t)kOptLds) o_bytes[ix(i)] = v; else sstore(9, i, v);
     }
     // the State of slot i's best path
-    template <bool F = false> FI uint32_t state_at(uint32_t i, uint32_t top) const { return RING ? bytes_at<F>(i, top) >> 24 : fs_at<F>(i) >> 4; }
+    template <bool F = false> FI uint32_t state_at(uint32_t i, uint32_t top) const { return bytes_at<F>(i, top) >> 24; }
     // RING: write back the ahead fields of slot i (its entry is about to hold i + 64)
     FI void evict_ahead(uint32_t i) {
         const uint32_t r = i & kOptMask;
-        LANE_FOR(uint32_t, k, 0u, 4u) {
-            const uint32_t v = k == 0 ? o_pp[r] : (k == 1 ? (uint32_t)o_bp[r] : (k == 2 ? (uint32_t)o_bp2[r] : (uint32_t)o_fs[r]));
+        LANE_FOR(uint32_t, k, 0u, 3u) {
+            const uint32_t v = k == 0 ? o_pp[r] : (k == 1 ? (uint32_t)o_bp[r] : (uint32_t)o_bp2[r]);
             sstore(1 + k, i, v);
         }
     }
     // RING: write back the behind fields of slot i
     FI void evict_behind(uint32_t i) {
         const uint32_t r = i & kOptMask;
-        LANE_FOR(uint32_t, k, 0u, 5u) sstore(5 + k, i, k < 4 ? o_backs[k * kOptLds + r] : o_bytes[r]);
+        LANE_FOR(uint32_t, k, 0u, 5u) sstore(5 + k, i, k < 4 ? o_backs[r * 4 + k] : o_bytes[r]);
     }
     // pair k of the current position's match list
     FI uint32_t md_l(uint32_t k) const { return PP::len(mdp[k]); }
     FI uint32_t md_d(uint32_t k) const { return PP::dist(mdp[k]); }
     FI uint32_t win_bytes() const { return g_cur | (g_mb << 8) | (g_prev << 16); }
-    template <bool F = false> FI uint32_t pos_prev(uint32_t i) const { return pp_at<F>(i) & 0xFFFFu; }
-    template <bool F = false> FI uint32_t pos_prev2(uint32_t i) const { return pp_at<F>(i) >> 16; }
+    template <bool F = false> FI uint32_t pos_prev(uint32_t i) const { return pp_at<F>(i) & kPosMask; }
+    template <bool F = false> FI uint32_t pos_prev2(uint32_t i) const { return (pp_at<F>(i) >> kPos2Shift) & kPosMask; }
     // after lanes wrote slots up to `hi`, make them visible to every lane
     FI void fence_upto(uint32_t hi) {
         LANE_FENCE();
@@ -387,6 +406,55 @@ struct Enc {
         return (uint32_t)__builtin_amdgcn_readfirstlane((int)price);
 #endif
     }
+#if LZG_EXP_LITPF
+    // issue the loads of position `pos`'s literal probabilities (coder after byte `prev`, symbol `sym`)
+    FI void lit_prefetch(uint32_t pos, uint32_t prev, uint32_t sym) {
+        const uint16_t* p = lit_coder(pos, prev);
+#pragma unroll
+        for (int t = 0; t < kLitSlots; t++) {
+#if LZG_WAVE == 64
+            const int i = 7 - (int)(lane & 7u);   // lanes 8-63 repeat lanes 0-7
+#else
+            const int i = 7 - (t * kWave + (int)lane);
+#endif
+            const uint32_t ctx = (0x100u | sym) >> (i + 1);
+            lpf0[t] = p[ctx]; lpf1[t] = p[0x100u + ctx]; lpf2[t] = p[0x200u + ctx];
+        }
+    }
+    // lit_price of the prefetched position (the same symbol): selects, no memory round trip
+    FI uint32_t lit_price_pf(bool match_mode, uint32_t mb, uint32_t sym) const {
+        int first = -1;
+        if (match_mode) {
+            uint32_t diff = (mb ^ sym) & 0xFFu;
+            first = diff ? 31 - __clz(diff) : -1;
+        }
+        uint32_t price = 0;
+#pragma unroll
+        for (int t = 0; t < kLitSlots; t++) {
+#if LZG_WAVE == 64
+            const int i = 7 - (int)(lane & 7u);
+#else
+            const int i = 7 - (t * kWave + (int)lane);
+#endif
+            const uint32_t bit = (sym >> i) & 1;
+            const uint32_t v = (match_mode && i >= first) ? (((mb >> i) & 1u) ? lpf2[t] : lpf1[t]) : lpf0[t];
+            const uint32_t pr = price_bit(v, bit);
+#if LZG_WAVE == 64
+            price = lane < 8 ? pr : 0u;
+#else
+            price += pr;
+#endif
+        }
+#if LZG_WAVE == 64
+        price += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)price, 0xB1, 0xF, 0xF, false);
+        price += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)price, 0x4E, 0xF, 0xF, false);
+        price += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)price, 0x12C, 0xF, 0xF, false);
+        return (uint32_t)__builtin_amdgcn_readlane((int)price, 0);
+#else
+        return (uint32_t)__builtin_amdgcn_readfirstlane((int)price);
+#endif
+    }
+#endif
     FI uint32_t len_price(int which, uint32_t sym, uint32_t ps) const {
         return lenp[(which << pb) * tsize + ps * tsize + sym];
     }
@@ -422,7 +490,6 @@ struct Enc {
     // bytes the position step prices its literal with in scalars and the cur side's
     // bytes in LDS (two-step literals). Compares past the window fall back to match_len.
     FI void gather(bool with_pairs) {
-        if (W2) { uint8_t* t = win; win = win_alt; win_alt = t; }   // B may still read the last position's bytes
         gp = mfpos - 1;
         const uint32_t d0 = rp0 + 1, d1 = rp1 + 1, d2 = rp2 + 1, d3 = rp3 + 1;
         const uint32_t e0 = num_pairs > 0 ? md_d(0) + 1 : d0, e1 = num_pairs > 1 ? md_d(1) + 1 : d0;
@@ -458,6 +525,7 @@ struct Enc {
         g_prev = lane_value(va, 0);
         g_cur = lane_value(va, 1);
         g_mb = lane_value(v0, 1);
+        g_next = lane_value(va, 2);
         LANE_FENCE();
     }
     // byte at p + o on the cur side
@@ -705,7 +773,7 @@ struct Enc {
     FI void ring_fill(uint32_t base) {
         ring_base = base;
         LANE_FOR(uint32_t, k, 0u, (uint32_t)kRing) {
-            const uint32_t e = W2 ? ((base + k) & (kRingN - 1)) : k;   // the ring entry of position base + k
+            const uint32_t e = k;
             uint32_t q = base + k;
             uint32_t info = 0;
             PairT p0 = 0, p1 = 0, p2 = 0, p3 = 0;
@@ -726,8 +794,7 @@ struct Enc {
         PBEGIN(t0);
         uint32_t q = mfpos;
         if (q - ring_base >= (uint32_t)kRing) ring_fill(q);
-        const uint32_t slot = W2 ? (q & (kRingN - 1)) : q - ring_base;
-        if (W2) { PairT* t = md_buf; md_buf = md_buf_alt; md_buf_alt = t; }   // B may still hold the last list
+        const uint32_t slot = q - ring_base;
         uint32_t info = ring_info[slot];
         uint32_t cnt = info & 0xFFFFu, ml = info >> 16;
         if (cnt <= (uint32_t)kInlinePairs) {   // read in place from the ring: no copy, no LDS round trip
@@ -784,7 +851,6 @@ struct Enc {
             if (hi > cur + (uint32_t)kOptLds) {   // cur + 65: its entry still holds cur + 1
                 far_valid = 1;
                 o_price[kFarEntry] = kInfinityPrice; o_pp[kFarEntry] = 0; o_bp[kFarEntry] = 0; o_bp2[kFarEntry] = 0;
-                o_fs[kFarEntry] = 0;
                 hi--;
             }
             if (hi >= (uint32_t)kOptLds) {   // entries reused: write back slots i - 64 first
@@ -793,7 +859,6 @@ struct Enc {
                     if (i >= (uint32_t)kOptLds) {
                         const uint32_t h = i - (uint32_t)kOptLds;
                         sstore(1, h, o_pp[r]); sstore(2, h, (uint32_t)o_bp[r]); sstore(3, h, (uint32_t)o_bp2[r]);
-                        sstore(4, h, (uint32_t)o_fs[r]);
                     }
                     o_price[r] = kInfinityPrice;
                 }
@@ -831,12 +896,10 @@ struct Enc {
                 const bool ok = l <= hi;
                 const uint32_t s = ok ? ix(base_slot + l) : (uint32_t)kOptLds;
                 const uint32_t cl = price_base + len_price(1, ok ? l - 2 : 0u, ps);
-                const uint32_t op = o_price[s], opp = o_pp[s], ofs = o_fs[s];
-                const uint32_t t = (ok && cl < op) ? s : (uint32_t)kOptLds;
+                const uint32_t t = (ok && cl < o_price[s]) ? s : (uint32_t)kOptLds;
                 o_price[t] = cl;
-                o_pp[t] = (opp & 0xFFFF0000u) | pos_prev_v;
+                o_pp[t] = pos_prev_v;   // Prev1IsChar = false (PosPrev2 / Prev2 are read only with it)
                 o_bp[t] = (int32_t)ri;
-                o_fs[t] = (uint8_t)(ofs & ~1u);
             }
             LANE_FENCE();
             return;
@@ -846,9 +909,8 @@ struct Enc {
             uint32_t s = base_slot + l;
             if (cl < price_at(s)) {
                 set_price(s, cl);
-                set_pp(s, (pp_at(s) & 0xFFFF0000u) | pos_prev_v);
+                set_pp(s, pos_prev_v);
                 set_bp(s, (int32_t)ri);
-                set_fs(s, fs_at(s) & ~1u);
             }
         }
         fence_upto(base_slot + hi);
@@ -862,12 +924,10 @@ struct Enc {
                 const bool ok = l <= hi;
                 const uint32_t s = ok ? ix(base_slot + l) : (uint32_t)kOptLds;
                 const uint32_t cl = price_base + pos_len_price(dist, ok ? l : (uint32_t)kMatchMinLen, ps);
-                const uint32_t op = o_price[s], opp = o_pp[s], ofs = o_fs[s];
-                const uint32_t t = (ok && cl < op) ? s : (uint32_t)kOptLds;
+                const uint32_t t = (ok && cl < o_price[s]) ? s : (uint32_t)kOptLds;
                 o_price[t] = cl;
-                o_pp[t] = (opp & 0xFFFF0000u) | pos_prev_v;
+                o_pp[t] = pos_prev_v;
                 o_bp[t] = (int32_t)(dist + kNumRepDistances);
-                o_fs[t] = (uint8_t)(ofs & ~1u);
             }
             LANE_FENCE();
             return;
@@ -877,9 +937,8 @@ struct Enc {
             uint32_t s = base_slot + l;
             if (cl < price_at(s)) {
                 set_price(s, cl);
-                set_pp(s, (pp_at(s) & 0xFFFF0000u) | pos_prev_v);
+                set_pp(s, pos_prev_v);
                 set_bp(s, (int32_t)(dist + kNumRepDistances));
-                set_fs(s, fs_at(s) & ~1u);
             }
         }
         fence_upto(base_slot + hi);
@@ -898,12 +957,10 @@ struct Enc {
                 const uint32_t distance = md_d(k);
                 const uint32_t s = ok ? l : (uint32_t)kOptLds;
                 const uint32_t cl = normal_match_price + pos_len_price(distance, ok ? l : (uint32_t)kMatchMinLen, pos_state);
-                const uint32_t op = o_price[s], opp = o_pp[s], ofs = o_fs[s];
-                const uint32_t t = (ok && cl < op) ? s : (uint32_t)kOptLds;
+                const uint32_t t = (ok && cl < o_price[s]) ? s : (uint32_t)kOptLds;
                 o_price[t] = cl;
-                o_pp[t] = opp & 0xFFFF0000u;
+                o_pp[t] = 0u;
                 o_bp[t] = (int32_t)(distance + kNumRepDistances);
-                o_fs[t] = (uint8_t)(ofs & ~1u);
             }
             LANE_FENCE();
             return;
@@ -915,9 +972,8 @@ struct Enc {
             uint32_t cl = normal_match_price + pos_len_price(distance, l, pos_state);
             if (cl < price_at<F>(l)) {
                 set_price<F>(l, cl);
-                set_pp<F>(l, pp_at<F>(l) & 0xFFFF0000u);
+                set_pp<F>(l, 0u);
                 set_bp<F>(l, (int32_t)(distance + kNumRepDistances));
-                set_fs<F>(l, fs_at<F>(l) & ~1u);
             }
         }
         if (F) LANE_FENCE(); else fence_upto(len_main);
@@ -928,12 +984,10 @@ struct Enc {
             set_price<F>(s, cl);
             set_bp<F>(s, 0);
             if (prev2) {
-                set_pp<F>(s, pos_prev_v | (pos_prev2_v << 16));
-                set_fs<F>(s, (fs_at<F>(s) & ~3u) | 3u);
+                set_pp<F>(s, pos_prev_v | (pos_prev2_v << kPos2Shift) | (3u << kFlagShift));
                 set_bp2<F>(s, back2);
             } else {
-                set_pp<F>(s, (pp_at<F>(s) & 0xFFFF0000u) | pos_prev_v);
-                set_fs<F>(s, (fs_at<F>(s) & ~3u) | 1u);
+                set_pp<F>(s, pos_prev_v | (1u << kFlagShift));
             }
         }
         fence_upto(s);
@@ -948,8 +1002,8 @@ struct Enc {
                 if (cl < o_price[e]) {
                     o_price[e] = cl;
                     o_bp[e] = 0;
-                    if (prev2) { o_pp[e] = pos_prev_v | (pos_prev2_v << 16); o_fs[e] = (uint8_t)((o_fs[e] & ~3u) | 3u); o_bp2[e] = back2; }
-                    else { o_pp[e] = (o_pp[e] & 0xFFFF0000u) | pos_prev_v; o_fs[e] = (uint8_t)((o_fs[e] & ~3u) | 1u); }
+                    if (prev2) { o_pp[e] = pos_prev_v | (pos_prev2_v << kPos2Shift) | (3u << kFlagShift); o_bp2[e] = back2; }
+                    else o_pp[e] = pos_prev_v | (1u << kFlagShift);
                 }
                 LANE_FENCE();
                 return;
@@ -972,12 +1026,10 @@ struct Enc {
             uint32_t fsc = fs_at<F>(cur);
             if (fsc & 1u) {
                 set_bp<F>(pos_mem, -1);
-                set_fs<F>(pos_mem, fs_at<F>(pos_mem) & ~1u);
-                set_pp<F>(pos_mem, (pp_at<F>(pos_mem) & 0xFFFF0000u) | (pos_mem - 1));
+                set_pp<F>(pos_mem, pos_mem - 1);   // MakeAsChar (Optimal.java:22-25): flags cleared
                 if (fsc & 2u) {
                     uint32_t m1 = pos_mem - 1;
-                    set_fs<F>(m1, fs_at<F>(m1) & ~1u);
-                    set_pp<F>(m1, (pp_at<F>(m1) & 0xFFFF0000u) | pos_prev2<F>(cur));
+                    set_pp<F>(m1, pos_prev2<F>(cur));
                     set_bp<F>(m1, bp2_at<F>(cur));
                 }
             }
@@ -986,7 +1038,7 @@ struct Enc {
             back_mem = bp_at<F>(ppv);
             pos_mem = pos_prev<F>(ppv);
             set_bp<F>(ppv, back_cur);
-            set_pp<F>(ppv, (pp_at<F>(ppv) & 0xFFFF0000u) | cur);
+            set_pp<F>(ppv, (pp_at<F>(ppv) & ~kPosMask) | cur);   // PosPrev = cur; ppv's flags stay
             cur = ppv;
         } while (cur > 0);
         opt_cur = (int32_t)pos_prev<F>(0);
@@ -1029,7 +1081,7 @@ struct Enc {
         PCOUNT(PF_NOPT);
         PBEGIN(t0);
         gather(false);
-        set_bytes<true>(0, win_bytes() | (RING ? state << 24 : 0u));
+        set_bytes<true>(0, win_bytes() | (state << 24));
         uint32_t num_avail = avail() + 1;
         if (num_avail < 2) { *back_res = -1; LANE_FENCE(); return 1; }
         if (num_avail > (uint32_t)kMatchMaxLen) num_avail = kMatchMaxLen;
@@ -1057,11 +1109,13 @@ struct Enc {
         uint32_t match_byte = g_mb;   // rp0 == rd0 here
         if (len_main < 2 && cur_byte != match_byte && rl_max < 2) { *back_res = -1; return 1; }
 
-        if (!RING) set_fs<true>(0, (fs_at<true>(0) & 0xFu) | (state << 4));
         uint32_t pos_state = position & ps_mask;
         PBEGIN(t1);
         uint32_t p1 = dm0(E_IS_MATCH + (state << PBS) + pos_state) +
                       lit_price(lit_coder(position, g_prev), !st_is_char(state), match_byte, cur_byte);
+#if LZG_EXP_LITPF
+        lit_prefetch(position + 1, cur_byte, g_next);   // the forward loop's first position
+#endif
         PEND(PF_LIT, t1);
         uint32_t match_price = dm1(E_IS_MATCH + (state << PBS) + pos_state);
         uint32_t rep_match_price = match_price + dm1(E_IS_REP + state);
@@ -1072,11 +1126,10 @@ struct Enc {
         }
         set_price<true>(1, p1);
         set_bp<true>(1, bp1);
-        set_fs<true>(1, fs_at<true>(1) & ~1u);
         uint32_t len_end = len_main >= rl_max ? len_main : rl_max;
         if (len_end < 2) { *back_res = bp1; LANE_FENCE(); return 1; }
-        set_pp<true>(1, pp_at<true>(1) & 0xFFFF0000u);
-        set_back<true>(0, 0, rp0); set_back<true>(0, 1, rp1); set_back<true>(0, 2, rp2); set_back<true>(0, 3, rp3);
+        set_pp<true>(1, 0u);
+        set_backs4<true>(0, rp0, rp1, rp2, rp3);
         LANE_FENCE();
         PBEGIN(t2);
         if (len_end < (uint32_t)kOptLds) {
@@ -1101,7 +1154,6 @@ struct Enc {
             else relax_first<false>(lstart, len_main, npairs, normal_match_price, pos_state);
         }
         PEND(PF_RELAX, t2);
-        if (W2) return parse_forward_w2(position, back_res, len_end);
         return parse_forward(position, back_res, len_end);
     }
 
@@ -1113,29 +1165,56 @@ struct Enc {
     // It is two parts: S (pos_state_part: the state, the reps, the gather and the literal
     // price of cur; reads slot cur and its predecessors, all final) and N (pos_next_part:
     // the literal / short-rep update of slot cur + 1, which cur - 1's longer candidates may
-    // have written). The two-wave kernel (W2) runs S of cur + 1 beside R of cur.
+    // have written).
     struct PosS { uint32_t st, pos_state, cur_price, cur_and1, cur_byte, match_byte; };
-    // COMMIT = false (W2): the slot writes wait for pos_commit, after the exit checks -- a
-    // speculative S of the pass's last slot must not overwrite the ring entry whose
-    // behind fields (slot cur - 64) the coder may still read
-    template <bool F, bool COMMIT = true>
+    template <bool F>
     FI PosS pos_state_part(uint32_t cur, uint32_t position) {
         PBEGIN(ts);
         // F: cur + 1 < kOptLds, every slot touched is in LDS. RING deep steps: the
         // ahead fields of cur and cur + 1 are in the ring (FA); the behind fields of
-        // pprev may be in HBM (a path back by 65), checked per access.
+        // the predecessor may be in HBM (a path back by 65), checked per access.
         constexpr bool FA = F || RING, FB = F;
         PosS r;
+#if LZG_EXP_BRANCHFREE_STATE
+        // slot cur's link (Encoder.java:518-535): one LDS round trip, then scalars
+        const uint32_t ppc = uni32(pp_at<FA>(cur));
+        const int32_t bpc = (int32_t)uni32((uint32_t)bp_at<FA>(cur));
+        const uint32_t fsc = ppc >> kFlagShift;
+        const bool c1 = (fsc & 1u) != 0, c2 = (fsc & 3u) == 3u;   // Prev1IsChar; Prev1IsChar && Prev2
+        // BackPrev2, meaningful with Prev2 only: read beside the others in LDS, on demand from HBM
+        const int32_t bp2c = FA ? (int32_t)uni32((uint32_t)bp2_at<FA>(cur)) : (c2 ? bp2_at<FA>(cur) : 0);
+        const uint32_t pp2 = (ppc >> kPos2Shift) & kPosMask;
+        const uint32_t pprev = (ppc & kPosMask) - (c1 ? 1u : 0u);
+        const bool lit_path = pprev == cur - 1;   // a literal or short rep from cur - 1: reps unchanged
+        // the slot both the start state and the Backs come from (PosPrev2 on a Prev2 path)
+        const uint32_t q = c2 ? pp2 : pprev;
+        const uint32_t sw = uni32(bytes_at<FB>(q, cur - 1));   // its byte record | State << 24
+        const v4u32 b = backs4_at<FB>(q, cur - 1);
+        // the state, branch-free (Encoder.java:520-555)
+        uint32_t st = sw >> 24;
+        st = c2 ? (bp2c < kNumRepDistances ? st_long(st) : st_match(st)) : st;
+        st = c1 ? st_lit(st) : st;
+        const int32_t pos = c2 ? bp2c : bpc;   // the last symbol's back on a non-literal path
+        st = lit_path ? (bpc == 0 ? st_short(st) : st_lit(st)) : ((c2 || pos < kNumRepDistances) ? st_long(st) : st_match(st));
+        // the reps (Encoder.java:556-584): a rep r moves Backs[r] to the front, a match
+        // shifts its distance in (the rep-3 pattern for reps 1..3)
+        const uint32_t b0 = uni32(b[0]), b1 = uni32(b[1]), b2 = uni32(b[2]), b3 = uni32(b[3]);
+        const int32_t r3 = pos < kNumRepDistances ? pos : 3;
+        const uint32_t n0 = pos < kNumRepDistances ? (pos == 0 ? b0 : (pos == 1 ? b1 : (pos == 2 ? b2 : b3)))
+                                                   : (uint32_t)(pos - kNumRepDistances);
+        const uint32_t n1 = r3 == 0 ? b1 : b0, n2 = r3 <= 1 ? b2 : b1, n3 = r3 <= 2 ? b3 : b2;
+        if (!lit_path) { rp0 = n0; rp1 = n1; rp2 = n2; rp3 = n3; }
+#else
         uint32_t st;
         uint32_t ppc = pp_at<FA>(cur);
-        uint32_t pos_prev_c = ppc & 0xFFFFu;
-        uint32_t fsc = fs_at<FA>(cur);
+        uint32_t pos_prev_c = ppc & kPosMask;
+        uint32_t fsc = ppc >> kFlagShift;
         int32_t bpc = bp_at<FA>(cur);
         uint32_t pprev = pos_prev_c;
         if (fsc & 1u) {
             pprev--;
             if (fsc & 2u) {
-                st = state_at<FB>(ppc >> 16, cur - 1);
+                st = state_at<FB>((ppc >> kPos2Shift) & kPosMask, cur - 1);
                 if (bp2_at<FA>(cur) < kNumRepDistances) st = st_long(st);
                 else st = st_match(st);
             } else st = state_at<FB>(pprev, cur - 1);
@@ -1147,7 +1226,7 @@ struct Enc {
         } else {
             int32_t pos;
             if ((fsc & 1u) && (fsc & 2u)) {
-                pprev = ppc >> 16;
+                pprev = (ppc >> kPos2Shift) & kPosMask;
                 pos = bp2_at<FA>(cur);
                 st = st_long(st);
             } else {
@@ -1155,8 +1234,8 @@ struct Enc {
                 if (pos < kNumRepDistances) st = st_long(st);
                 else st = st_match(st);
             }
-            uint32_t b0 = back_at<FB>(pprev, 0, cur - 1), b1 = back_at<FB>(pprev, 1, cur - 1), b2 = back_at<FB>(pprev, 2, cur - 1),
-                     b3 = back_at<FB>(pprev, 3, cur - 1);
+            const v4u32 b = backs4_at<FB>(pprev, cur - 1);
+            const uint32_t b0 = b[0], b1 = b[1], b2 = b[2], b3 = b[3];
             if (pos < kNumRepDistances) {
                 if (pos == 0) { rp0 = b0; rp1 = b1; rp2 = b2; rp3 = b3; }
                 else if (pos == 1) { rp0 = b1; rp1 = b0; rp2 = b2; rp3 = b3; }
@@ -1166,38 +1245,36 @@ struct Enc {
                 rp0 = (uint32_t)(pos - kNumRepDistances); rp1 = b0; rp2 = b1; rp3 = b2;
             }
         }
-        if (COMMIT) {
-            if (RING) {   // cur's entry held cur - 64
-                if (!F && cur >= (uint32_t)kOptLds) evict_behind(cur - (uint32_t)kOptLds);
-            } else set_fs<FA>(cur, (fsc & 0xFu) | (st << 4));
-            set_back<FA>(cur, 0, rp0); set_back<FA>(cur, 1, rp1); set_back<FA>(cur, 2, rp2); set_back<FA>(cur, 3, rp3);
+#endif
+        if (RING) {   // cur's entry held cur - 64
+            if (!F && cur >= (uint32_t)kOptLds) evict_behind(cur - (uint32_t)kOptLds);
         }
+        set_backs4<FA>(cur, rp0, rp1, rp2, rp3);
         r.cur_price = price_at<FA>(cur);
         r.pos_state = position & ps_mask;
         r.st = st;
         PEND(PF_STATE, ts);
         return r;
     }
-    template <bool F, bool COMMIT = true>
+    template <bool F>
     FI void pos_gather_part(uint32_t cur, uint32_t position, PosS& r) {
         constexpr bool FA = F || RING;
         PBEGIN(tg);
         gather(true);
-        if (COMMIT) set_bytes<FA>(cur, win_bytes() | (RING ? r.st << 24 : 0u));
+        set_bytes<FA>(cur, win_bytes() | (r.st << 24));
         PEND(PF_REPLEN, tg);
         r.cur_byte = g_cur;
         r.match_byte = g_mb;
         PBEGIN(tl);
+#if LZG_EXP_LITPF
+        r.cur_and1 = r.cur_price + dm0(E_IS_MATCH + (r.st << PBS) + r.pos_state) +
+                     lit_price_pf(!st_is_char(r.st), r.match_byte, r.cur_byte);
+        lit_prefetch(position + 1, r.cur_byte, g_next);   // for cur + 1, under this step's relaxations
+#else
         r.cur_and1 = r.cur_price + dm0(E_IS_MATCH + (r.st << PBS) + r.pos_state) +
                      lit_price(lit_coder(position, g_prev), !st_is_char(r.st), r.match_byte, r.cur_byte);
+#endif
         PEND(PF_LIT, tl);
-    }
-    // W2 (RING only): the slot writes S deferred, once the step is known to run
-    template <bool F>
-    FI void pos_commit(uint32_t cur, const PosS& r) {
-        if (!F && cur >= (uint32_t)kOptLds) evict_behind(cur - (uint32_t)kOptLds);
-        set_back<true>(cur, 0, rp0); set_back<true>(cur, 1, rp1); set_back<true>(cur, 2, rp2); set_back<true>(cur, 3, rp3);
-        set_bytes<true>(cur, win_bytes() | (r.st << 24));
     }
     // N: slot cur + 1's literal and short-rep candidates (nx_*: its fields, read by the caller)
     template <bool F>
@@ -1208,16 +1285,16 @@ struct Enc {
         const uint32_t nx = cur + 1, st = r.st, pos_state = r.pos_state;
         bool next_is_char = false;
         if (r.cur_and1 < nx_price) {
-            nx_price = r.cur_and1; nx_pp = (nx_pp & 0xFFFF0000u) | cur; nx_bp = -1;
-            set_price<FA>(nx, nx_price); set_pp<FA>(nx, nx_pp); set_bp<FA>(nx, -1); set_fs<FA>(nx, fs_at<FA>(nx) & ~1u);
+            nx_price = r.cur_and1; nx_pp = cur; nx_bp = -1;
+            set_price<FA>(nx, nx_price); set_pp<FA>(nx, nx_pp); set_bp<FA>(nx, -1);
             next_is_char = true;
         }
         match_price = r.cur_price + dm1(E_IS_MATCH + (st << PBS) + pos_state);
         rep_match_price = match_price + dm1(E_IS_REP + st);
-        if (r.match_byte == r.cur_byte && !((nx_pp & 0xFFFFu) < cur && nx_bp == 0)) {
+        if (r.match_byte == r.cur_byte && !((nx_pp & kPosMask) < cur && nx_bp == 0)) {
             uint32_t srp = rep_match_price + rep_len1_price(st, pos_state);
             if (srp <= nx_price) {
-                set_price<FA>(nx, srp); set_pp<FA>(nx, (nx_pp & 0xFFFF0000u) | cur); set_bp<FA>(nx, 0); set_fs<FA>(nx, fs_at<FA>(nx) & ~1u);
+                set_price<FA>(nx, srp); set_pp<FA>(nx, cur); set_bp<FA>(nx, 0);
                 next_is_char = true;
             }
         }
@@ -1248,9 +1325,9 @@ struct Enc {
         if (RING && far_valid) {   // slot cur + 64 leaves the far entry for cur's, free now
             evict_ahead(cur);
             const uint32_t rr = cur & kOptMask, e = kFarEntry;
-            const uint32_t fp = o_price[e], fpp = o_pp[e], ffs = o_fs[e];
+            const uint32_t fp = o_price[e], fpp = o_pp[e];
             const int32_t fbp = o_bp[e], fbp2 = o_bp2[e];
-            o_price[rr] = fp; o_pp[rr] = fpp; o_bp[rr] = fbp; o_bp2[rr] = fbp2; o_fs[rr] = (uint8_t)ffs;
+            o_price[rr] = fp; o_pp[rr] = fpp; o_bp[rr] = fbp; o_bp2[rr] = fbp2;
             ring_top = cur + (uint32_t)kOptLds;
             far_valid = 0;
             LANE_FENCE();
@@ -1382,11 +1459,37 @@ struct Enc {
         }
     }
 
+    FI void park() {
+        Cold* c = cold;
+        c->recs = (uint64_t)recs; c->rcap = rcap; c->rpos = rpos;
+        c->rd0 = rd0; c->rd1 = rd1; c->rd2 = rd2; c->rd3 = rd3;
+        c->state = state; c->prev_byte = prev_byte; c->mpc = match_price_count; c->apc = align_price_count;
+        c->overflow = overflow; c->dts = dist_table_size;
+        LANE_FENCE();   // a compiler memory barrier: unpark's loads are not forwarded from these stores
+    }
+    FI void unpark() {
+        LANE_FENCE();
+        const Cold* c = cold;
+        recs = (uint16_t*)uni64(c->recs); rcap = uni64(c->rcap); rpos = uni64(c->rpos);
+        rd0 = uni32(c->rd0); rd1 = uni32(c->rd1); rd2 = uni32(c->rd2); rd3 = uni32(c->rd3);
+        state = uni32(c->state); prev_byte = uni32(c->prev_byte);
+        match_price_count = uni32(c->mpc); align_price_count = uni32(c->apc);
+        overflow = uni32(c->overflow); dist_table_size = uni32(c->dts);
+    }
     FI uint32_t parse_forward(uint32_t position, int32_t* back_res, uint32_t len_end) {
+#if LZG_EXP_PARK
+        park();
+        const uint32_t len = parse_forward_loop(position, back_res, len_end);
+        unpark();
+        return len;
+#else
+        return parse_forward_loop(position, back_res, len_end);
+#endif
+    }
+    FI uint32_t parse_forward_loop(uint32_t position, int32_t* back_res, uint32_t len_end) {
         uint32_t cur = 0;
         DBG(5, len_end);
         for (;;) {
-            WDOG(3);
             cur++;
             DBG(6, cur);
             if (bad) { *back_res = -1; return 1; }
@@ -1412,132 +1515,6 @@ struct Enc {
             relax_step(cur, position, r, next_is_char, match_price, rep_match_price, new_len, npairs, len_end);
         }
         __builtin_unreachable();   // the loop returns
-    }
-
-    // ------------------------------------------------------------ two-wave parse (W2)
-    FI void pipe_sync() { __syncthreads(); }   // one workgroup barrier (both waves)
-    // A: hand R(cur) to B (ctrl kPipeRelax), or stop B (kPipeIdle / kPipeExit)
-    FI void publish(uint32_t ctrl, uint32_t cur, uint32_t position, const PosS& r, bool next_is_char, uint32_t match_price,
-                    uint32_t rep_match_price, uint32_t new_len, uint32_t npairs, uint32_t len_end) {
-        Pipe* P = pipe;
-        P->ctrl = ctrl;
-        P->len_end = len_end; P->ring_top = ring_top; P->far_valid = far_valid; P->bad = bad;
-        if (ctrl == kPipeRelax) {
-            P->cur = cur; P->position = position; P->st = r.st; P->pos_state = r.pos_state; P->cur_and1 = r.cur_and1;
-            P->cur_byte = r.cur_byte; P->match_byte = r.match_byte;
-            P->next_is_char = next_is_char ? 1u : 0u; P->match_price = match_price; P->rep_match_price = rep_match_price;
-            P->new_len = new_len; P->npairs = npairs;
-            P->gp = gp; P->mfpos = mfpos;
-            P->md_off = (uint32_t)((const uint8_t*)mdp - lds_base); P->mdbuf_off = (uint32_t)((uint8_t*)md_buf - lds_base);
-            P->win_off = (uint32_t)(win - lds_base);
-            P->rp0 = rp0; P->rp1 = rp1; P->rp2 = rp2; P->rp3 = rp3;
-            P->gm0 = gm0; P->gm1 = gm1; P->gm2 = gm2; P->gm3 = gm3; P->gmp0 = gmp0; P->gmp1 = gmp1;
-        }
-        LANE_FENCE();
-    }
-    // A: the forward loop of getOptimum with R on wave B (same slot updates, same order:
-    // R(c) ends before N(c + 1) starts, and S(c + 1) reads only slots R(c) never writes)
-    FI uint32_t parse_forward_w2(uint32_t position, int32_t* back_res, uint32_t len_end) {
-        uint32_t cur = 1;
-        if (++wd > wd_max) bad = 103;
-        if (bad) { *back_res = -1; return 1; }
-        if (cur == len_end) return backward(back_res, cur);
-        if (len_end >= (uint32_t)kNumOpts) { bad = 4; *back_res = -1; return 1; }
-        uint32_t new_len = read_match_distances();
-        if (new_len >= fb) {
-            longest_len = new_len;
-            longest_found = 1;
-            return backward(back_res, cur);
-        }
-        position++;
-        PosS r;
-        uint32_t match_price, rep_match_price;
-        bool next_is_char = pos_step<true>(cur, position, r, match_price, rep_match_price);   // cur + 1 = 2 < kOptLds
-        // A writes the record only between P and Q: B reads it right after Q, and by the next
-        // P it is done with it (here: B's read of the last pass's kPipeIdle)
-        pipe_sync();   // P
-        publish(kPipeRelax, cur, position, r, next_is_char, match_price, rep_match_price, new_len, num_pairs, len_end);
-        pipe_sync();   // Q: B runs R(cur)
-        for (;;) {
-            // S(cur + 1), speculative: the exit checks need R(cur)'s len_end
-            const uint32_t nc = cur + 1;
-            const uint32_t sv_mfpos = mfpos;
-            const int32_t sv_addoff = additional_offset;
-            const bool spec = nc < (uint32_t)kNumOpts - 1;
-            uint32_t nnew = 0;
-            PosS nr{};
-            if (spec) {
-                nnew = read_match_distances();
-                if (nnew < fb) {
-                    if (nc + 1 < (uint32_t)kOptLds) { nr = pos_state_part<true, false>(nc, position + 1); pos_gather_part<true, false>(nc, position + 1, nr); }
-                    else { nr = pos_state_part<false, false>(nc, position + 1); pos_gather_part<false, false>(nc, position + 1, nr); }
-                }
-            }
-            pipe_sync();   // P: R(cur) is done
-            {
-                const Pipe* P = pipe;
-                len_end = P->len_end; ring_top = P->ring_top; far_valid = P->far_valid;
-                if (P->bad && !bad) bad = P->bad;
-            }
-            cur = nc;
-            if (++wd > wd_max && !bad) bad = 103;
-            int32_t ret_back = -1;
-            uint32_t ret = 0;   // 0: the step runs; else the value getOptimum returns
-            if (bad) ret = 1;
-            else if (cur == len_end) {   // the pass ends before this position's read: undo it
-                if (spec) { mfpos = sv_mfpos; additional_offset = sv_addoff; }
-                ret = 2;
-            } else if (cur >= (uint32_t)kNumOpts - 1 || len_end >= (uint32_t)kNumOpts) { bad = 4; ret = 1; }
-            else if (nnew >= fb) { longest_len = nnew; longest_found = 1; ret = 2; }
-            if (ret) {
-                publish(kPipeIdle, 0, 0, r, false, 0, 0, 0, 0, len_end);
-                pipe_sync();   // Q: B goes back to wait
-                if (ret == 2) return backward(back_res, cur);
-                *back_res = ret_back;
-                return 1;
-            }
-            position++;
-            new_len = nnew;
-            // N(cur): slot cur + 1, now that R(cur - 1) is done
-            const uint32_t nx = cur + 1;
-            const uint32_t nx_price = price_at<true>(nx), nx_pp = pp_at<true>(nx);
-            const int32_t nx_bp = bp_at<true>(nx);
-            if (nx < (uint32_t)kOptLds) { pos_commit<true>(cur, nr); next_is_char = pos_next_part<true>(cur, nr, nx_price, nx_pp, nx_bp, match_price, rep_match_price); }
-            else { pos_commit<false>(cur, nr); next_is_char = pos_next_part<false>(cur, nr, nx_price, nx_pp, nx_bp, match_price, rep_match_price); }
-            r = nr;
-            publish(kPipeRelax, cur, position, r, next_is_char, match_price, rep_match_price, new_len, num_pairs, len_end);
-            pipe_sync();   // Q: B runs R(cur)
-        }
-    }
-    // B: waits for R steps until A stops it
-    FI void relax_wave() {
-        for (;;) {
-            pipe_sync();   // P
-            pipe_sync();   // Q
-            const Pipe* P = pipe;
-            const uint32_t ctrl = P->ctrl;
-            if (ctrl == kPipeExit) return;
-            if (ctrl != kPipeRelax) continue;
-            PosS r;
-            const uint32_t cur = P->cur, position = P->position;
-            r.st = P->st; r.pos_state = P->pos_state; r.cur_and1 = P->cur_and1; r.cur_byte = P->cur_byte;
-            r.match_byte = P->match_byte; r.cur_price = 0;
-            const bool next_is_char = P->next_is_char != 0;
-            const uint32_t match_price = P->match_price, rep_match_price = P->rep_match_price;
-            const uint32_t new_len = P->new_len, npairs = P->npairs;
-            gp = P->gp; mfpos = P->mfpos;
-            mdp = (const PairT*)(lds_base + P->md_off);
-            md_buf = (PairT*)(lds_base + P->mdbuf_off);
-            win = lds_base + P->win_off;
-            rp0 = P->rp0; rp1 = P->rp1; rp2 = P->rp2; rp3 = P->rp3;
-            gm0 = (GM)P->gm0; gm1 = (GM)P->gm1; gm2 = (GM)P->gm2; gm3 = (GM)P->gm3; gmp0 = (GM)P->gmp0; gmp1 = (GM)P->gmp1;
-            uint32_t len_end = P->len_end;
-            ring_top = P->ring_top; far_valid = P->far_valid; bad = 0;
-            relax_step(cur, position, r, next_is_char, match_price, rep_match_price, new_len, npairs, len_end);
-            Pipe* W = pipe;
-            W->len_end = len_end; W->ring_top = ring_top; W->far_valid = far_valid; W->bad = bad;
-            LANE_FENCE();
-        }
     }
 
     // ------------------------------------------------------------ emitters (Encoder.java:860-1024, 818-841)
@@ -1622,7 +1599,6 @@ struct Enc {
         rd0 = rd1 = rd2 = rd3 = 0;
         rp0 = rp1 = rp2 = rp3 = 0;
         rpos = 0; overflow = 0; bad = 0;
-        wd = 0; wd_max = n < 0x50000000u ? 3 * n + 4096 : 0xFFFFFFFFu;   // iterations <= 2n + calls
         longest_found = 0; opt_end = 0; opt_cur = 0; additional_offset = 0;
         longest_len = 0; num_pairs = 0; mfpos = 0;
         ring_base = 0x80000000u;   // force a fill at the first read (streams < 2 GiB)
@@ -1636,7 +1612,7 @@ struct Enc {
         DBG(1, 4);
 
         uint32_t now_pos = 0;
-        prio.start(g_enc_sched, n, lane);
+        cold->prio.start(g_enc_sched, n, lane);
         if (avail() == 0) { flush(0); return; }
         read_match_distances();
         DBG(1, 5);
@@ -1646,7 +1622,6 @@ struct Enc {
         if (avail() == 0) { flush(now_pos); return; }
         DBG(1, 6);
         for (;;) {
-            WDOG(4);
             int32_t back;
             DBG(2, now_pos);
             DBG(3, mfpos);
@@ -1684,7 +1659,7 @@ struct Enc {
                 if (match_price_count >= (1u << 7)) fill_distances_prices();
                 if (align_price_count >= (uint32_t)kAlignTableSize) fill_align_prices();
                 PEND(PF_TABLES, tt);
-                prio.update(now_pos, lane);
+                cold->prio.update(now_pos, lane);
                 if (avail() == 0) { flush(now_pos); return; }
             }
         }
@@ -1694,33 +1669,41 @@ struct Enc {
 // LDS layout of one stream's workgroup; shared by the kernel (carving) and
 // the host (dynamic LDS size). Regions are 16-byte aligned.
 enum { L_PP, L_PROBS, L_DMP, L_LENP, L_LENC, L_PSP, L_DP, L_AP, L_TP, L_MDBUF, L_RINFO, L_RPAIRS, L_OPRICE,
-       L_OPP, L_OBP, L_OBP2, L_OFS, L_OBACKS, L_OBYTES, L_TPBUF, L_RBUF, L_LIT, L_PIPE, L_MDBUF2, L_WIN2, L_COUNT };
-__host__ __device__ inline uint32_t enc_lds_layout(const EncArgs& a, uint32_t* off) {
-    const uint32_t md_cap = a.fb + 2;   // pairs per position <= fb (+1 clamp slot)
+       L_OPP, L_OBP, L_OBP2, L_OBACKS, L_OBYTES, L_TPBUF, L_RBUF, L_COLD, L_LIT, L_COUNT };
+__host__ __device__ constexpr uint32_t enc_lds_layout_p(uint32_t fb, uint32_t pb, uint32_t lc, uint32_t lp, uint32_t lit_in_lds,
+                                                      uint32_t pair_bytes, uint32_t len_table_size, uint32_t* off) {
+    const uint32_t md_cap = fb + 2;   // pairs per position <= fb (+1 clamp slot)
     const uint32_t sz[L_COUNT] = {
-        512 * 2, prob_count(a.pb) * 2 + 2, dm_count(a.pb) * 4 + 4, 2 * (1u << a.pb) * a.len_table_size * 2, 2 * 16 * 4, 256 * 2, 512 * 2, 16 * 4,
-        0u /* L_TP: unused (tempPrices are L_TPBUF) */, md_cap * a.pair_bytes, (a.w2 ? 2u : 1u) * kRing * 4,
-        (a.w2 ? 2u : 1u) * kRing * kInlinePairs * a.pair_bytes,
-        (kOptLds + 2) * 4, (kOptLds + 2) * 4, (kOptLds + 2) * 4, (kOptLds + 2) * 4, kOptLds + 2, 4 * kOptLds * 4, kOptLds * 4, kTpBytes, kRbuf * 2 + 2,
-        a.lit_in_lds ? (0x300u << (a.lc + a.lp)) * 2 + 2 : 0u,
-        a.w2 ? (uint32_t)sizeof(Pipe) : 0u, a.w2 ? md_cap * a.pair_bytes : 0u, a.w2 ? (uint32_t)kGW : 0u};
+        512 * 2, prob_count(pb) * 2 + 2, dm_count(pb) * 4 + 4, 2 * (1u << pb) * len_table_size * 2, 2 * 16 * 4, 256 * 2, 512 * 2, 16 * 4,
+        0u /* L_TP: unused (tempPrices are L_TPBUF) */, md_cap * pair_bytes, kRing * 4,
+        kRing * kInlinePairs * pair_bytes,
+        (kOptLds + 2) * 4, (kOptLds + 2) * 4, (kOptLds + 2) * 4, (kOptLds + 2) * 4, 4 * kOptLds * 4, kOptLds * 4, kTpBytes, kRbuf * 2 + 2, 128u /* Enc::Cold */,
+        lit_in_lds ? (0x300u << (lc + lp)) * 2 + 2 : 0u};
     uint32_t o = 0;
     for (int i = 0; i < L_COUNT; i++) { if (off) off[i] = o; o += (sz[i] + 15) & ~15u; }
     return o;
 }
+__host__ __device__ inline uint32_t enc_lds_layout(const EncArgs& a, uint32_t* off) {
+    return enc_lds_layout_p(a.fb, a.pb, a.lc, a.lp, a.lit_in_lds, a.pair_bytes, a.len_table_size, off);
+}
+// the bench parameters' layout (SPEC = 1: fb 32, lc 3, lp 0, pb 2), by pair width and literal-coder placement
+template <int PAIR_BYTES, bool LIT>
+constexpr uint32_t kSpec1LdsBytes = enc_lds_layout_p(32, 2, 3, 0, LIT ? 1u : 0u, PAIR_BYTES, 31, nullptr);
 
 // SPEC = 1: the level-5 parameters of bench.py (fb 32, lc 3, lp 0, pb 2, no end
 // marker) as compile-time constants; SPEC = 2: any parameters with fb <= 32;
 // SPEC = 0: fb > 32. SPEC 1 and 2 keep _optimum in the LDS ring.
-// W2 (SPEC 1 and 2 only): two waves per stream (Enc::parse_forward_w2 / relax_wave), for
-// launches with few streams per CU; their register budget is 256 per lane (2 waves per SIMD).
-template <typename PairT, bool LIT_LDS, int PBS, int SPEC, bool W2 = false>
-__global__ void __launch_bounds__(W2 ? 2 * kWave : kWave, W2 ? 2 : 4) enc_kernel(EncArgs a) {
+template <typename PairT, bool LIT_LDS, int PBS, int SPEC>
+__global__ void __launch_bounds__(kWave, 4) enc_kernel(EncArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    static_assert(!W2 || SPEC != 0, "the two-wave parse needs the _optimum ring (fb <= 32)");
-    Enc<PairT, LIT_LDS, PBS, (SPEC != 0), W2> e;   // SPEC 1 and 2: fb <= 32, the _optimum ring
-    // the wave index is wave-uniform: readfirstlane makes that visible (scalar branches on it)
-    const uint32_t wave = W2 ? (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave)) : 0u;
+    uint8_t* sm = smem;
+#if LZG_EXP_STATIC_LDS
+    // SPEC 1: a static array, so every LDS offset folds into its ds instruction (other
+    // kernels: a 16-byte placeholder, the dynamic array is theirs)
+    __shared__ __attribute__((aligned(16))) uint8_t smem_s[SPEC == 1 ? kSpec1LdsBytes<(int)sizeof(PairT), LIT_LDS> : 16u];
+    if constexpr (SPEC == 1) sm = smem_s;
+#endif
+    Enc<PairT, LIT_LDS, PBS, (SPEC != 0)> e;   // SPEC 1 and 2: fb <= 32, the _optimum ring
     e.lane = threadIdx.x % kWave;
     if (SPEC == 1) {
         e.fb = 32; e.lc = 3; e.lp = 0; e.pb = 2; e.ps_mask = 3; e.eos = 0; e.tsize = 31;
@@ -1732,45 +1715,37 @@ __global__ void __launch_bounds__(W2 ? 2 * kWave : kWave, W2 ? 2 : 4) enc_kernel
     uint32_t off[L_COUNT];
     {
         EncArgs la = a;   // SPEC: the layout folds to constants (immediate LDS offsets, no SGPR per region)
-        if (SPEC == 1) { la.fb = 32; la.pb = 2; la.lc = 3; la.lp = 0; la.lit_in_lds = LIT_LDS ? 1 : 0; la.pair_bytes = 4; la.len_table_size = 31; }
-        la.w2 = W2 ? 1u : 0u;
+        if (SPEC == 1) { la.fb = 32; la.pb = 2; la.lc = 3; la.lp = 0; la.lit_in_lds = LIT_LDS ? 1 : 0; la.pair_bytes = (uint32_t)sizeof(PairT); la.len_table_size = 31; }
         enc_lds_layout(la, off);
     }
-    e.pp = (uint16_t*)(smem + off[L_PP]);
-    e.probs = (uint16_t*)(smem + off[L_PROBS]);
-    e.lenp = (uint16_t*)(smem + off[L_LENP]);
-    e.lenc = (uint32_t*)(smem + off[L_LENC]);
-    e.psp = (uint16_t*)(smem + off[L_PSP]);
-    e.dp = (uint16_t*)(smem + off[L_DP]);
-    e.ap = (uint32_t*)(smem + off[L_AP]);
-    e.tp = (uint16_t*)(smem + off[L_TPBUF]);   // tempPrices (FillDistancesPrices' scratch), aliasing the window
-    e.win = smem + off[L_TPBUF];
-    e.dmp = (uint32_t*)(smem + off[L_DMP]);
-    e.md_buf = (PairT*)(smem + off[L_MDBUF]);
+    e.pp = (uint16_t*)(sm + off[L_PP]);
+    e.probs = (uint16_t*)(sm + off[L_PROBS]);
+    e.lenp = (uint16_t*)(sm + off[L_LENP]);
+    e.lenc = (uint32_t*)(sm + off[L_LENC]);
+    e.psp = (uint16_t*)(sm + off[L_PSP]);
+    e.dp = (uint16_t*)(sm + off[L_DP]);
+    e.ap = (uint32_t*)(sm + off[L_AP]);
+    e.tp = (uint16_t*)(sm + off[L_TPBUF]);   // tempPrices (FillDistancesPrices' scratch), aliasing the window
+    e.win = sm + off[L_TPBUF];
+    e.dmp = (uint32_t*)(sm + off[L_DMP]);
+    e.md_buf = (PairT*)(sm + off[L_MDBUF]);
     e.mdp = e.md_buf;
-    e.ring_info = (uint32_t*)(smem + off[L_RINFO]);
-    e.ring_pairs = (PairT*)(smem + off[L_RPAIRS]);
-    e.o_price = (uint32_t*)(smem + off[L_OPRICE]);
-    e.o_pp = (uint32_t*)(smem + off[L_OPP]);
-    e.o_bp = (int32_t*)(smem + off[L_OBP]);
-    e.o_bp2 = (int32_t*)(smem + off[L_OBP2]);
-    e.o_fs = smem + off[L_OFS];
-    e.o_backs = (uint32_t*)(smem + off[L_OBACKS]);
-    e.o_bytes = (uint32_t*)(smem + off[L_OBYTES]);
-    e.rbuf = (uint16_t*)(smem + off[L_RBUF]);
-    if (W2) {
-        e.lds_base = smem;
-        e.pipe = (Pipe*)(smem + off[L_PIPE]);
-        e.md_buf_alt = (PairT*)(smem + off[L_MDBUF2]);
-        e.win_alt = smem + off[L_WIN2];
-    }
+    e.ring_info = (uint32_t*)(sm + off[L_RINFO]);
+    e.ring_pairs = (PairT*)(sm + off[L_RPAIRS]);
+    e.o_price = (uint32_t*)(sm + off[L_OPRICE]);
+    e.o_pp = (uint32_t*)(sm + off[L_OPP]);
+    e.o_bp = (int32_t*)(sm + off[L_OBP]);
+    e.o_bp2 = (int32_t*)(sm + off[L_OBP2]);
+    e.o_backs = (uint32_t*)(sm + off[L_OBACKS]);
+    e.o_bytes = (uint32_t*)(sm + off[L_OBYTES]);
+    e.rbuf = (uint16_t*)(sm + off[L_RBUF]);
+    e.cold = (typename Enc<PairT, LIT_LDS, PBS, (SPEC != 0)>::Cold*)(sm + off[L_COLD]);
     uint8_t* scratch = a.scratch + (size_t)blockIdx.x * a.scratch_stride;
     e.spill = __builtin_amdgcn_make_buffer_rsrc(scratch, 0, kNumOpts * 4 * 10, 0x00020000);
     uint16_t* lit_g = (uint16_t*)(a.lit_scratch + (size_t)blockIdx.x * a.lit_stride);
-    if (LIT_LDS) e.lit = (uint16_t*)(smem + off[L_LIT]);
+    if (LIT_LDS) e.lit = (uint16_t*)(sm + off[L_LIT]);
     else e.lit = lit_g;
-    if (wave == 0)
-        for (int i0 = 0; i0 < 512; i0 += kWave) e.pp[i0 + e.lane] = (uint16_t)c_tab.prices[i0 + e.lane];
+    for (int i0 = 0; i0 < 512; i0 += kWave) e.pp[i0 + e.lane] = (uint16_t)c_tab.prices[i0 + e.lane];
     LANE_FENCE();
     e.dbg = a.dbg;
 #ifdef LZG_DEBUG
@@ -1787,7 +1762,7 @@ __global__ void __launch_bounds__(W2 ? 2 * kWave : kWave, W2 ? 2 : 4) enc_kernel
     const int s = __builtin_amdgcn_readfirstlane((int)a.order[blockIdx.x]);
     if (s < 0 || s >= a.nstreams) return;   // a corrupt order entry: touch nothing (the host checked the order it wrote)
     if (uni64(a.offs[s + 1]) < uni64(a.offs[s]) || uni64(a.rec_offs[s + 1]) < uni64(a.rec_offs[s])) {
-        if (wave == 0 && e.lane == 0) { a.rec_lens[s] = 0; a.out_lens[s] = 9ull << 32; a.status[s] = LZMA_E_INTERNAL; }
+        if (e.lane == 0) { a.rec_lens[s] = 0; a.out_lens[s] = 9ull << 32; a.status[s] = LZMA_E_INTERNAL; }
         return;
     }
     e.gbase = uni64(a.offs[s]);
@@ -1800,22 +1775,12 @@ __global__ void __launch_bounds__(W2 ? 2 * kWave : kWave, W2 ? 2 : 4) enc_kernel
 #ifdef LZG_DEBUG
     if (e.dbg && e.lane == 0) __hip_atomic_store(e.dbg + 8, (uint32_t)s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 #endif
-    if (W2 && wave == 1) {   // B: relax steps until A's exit
-        e.relax_wave();
-        return;
-    }
 #ifdef LZG_PROF
     const uint64_t t_run = __builtin_amdgcn_s_memtime();
     const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
 #endif
     e.run();
-    e.prio.finish(e.lane);
-    if (W2) {   // B waits at a barrier pair for its next step: release it
-        typename Enc<PairT, LIT_LDS, PBS, (SPEC != 0), W2>::PosS r0{};
-        e.pipe_sync();   // P
-        e.publish(kPipeExit, 0, 0, r0, false, 0, 0, 0, 0, 0);
-        e.pipe_sync();   // Q
-    }
+    e.cold->prio.finish(e.lane);
 #ifdef LZG_PROF
     e.prof[PF_TOTAL] = __builtin_amdgcn_s_memtime() - t_run;
     e.prof[PF_T0] = rt0;   // 100 MHz wall clock: where each stream ran
@@ -1852,14 +1817,7 @@ int enc_grid(const Derived&, int nstreams) { return nstreams; }   // one workgro
 template <typename PairT, bool LIT, int PBS, int SPEC>
 static void launch_spec(Ctx* ctx, const EncArgs& a, int grid, size_t lds, hipStream_t st) {
     TimedLaunch tl(ctx, "enc_parse", st);
-    if constexpr (SPEC != 0) {
-        if (a.w2) {
-            if (lds > 64 * 1024)
-                hipFuncSetAttribute((const void*)enc_kernel<PairT, LIT, PBS, SPEC, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-            hipLaunchKernelGGL((enc_kernel<PairT, LIT, PBS, SPEC, true>), dim3(grid), dim3(2 * kWave), lds, st, a);
-            return;
-        }
-    }
+    if (LZG_EXP_STATIC_LDS && SPEC == 1) lds = 0;   // the kernel's static array
     if (lds > 64 * 1024)
         hipFuncSetAttribute((const void*)enc_kernel<PairT, LIT, PBS, SPEC>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL((enc_kernel<PairT, LIT, PBS, SPEC>), dim3(grid), dim3(kWave), lds, st, a);
@@ -1867,7 +1825,7 @@ static void launch_spec(Ctx* ctx, const EncArgs& a, int grid, size_t lds, hipStr
 
 template <typename PairT, bool LIT, int PBS>
 static void launch_one(Ctx* ctx, const EncArgs& a, int grid, size_t lds, hipStream_t st) {
-    if constexpr (std::is_same<PairT, uint32_t>::value && PBS == 2) {
+    if constexpr (PBS == 2) {   // both pair widths: a single stream >= 8 MiB (config 4) takes the u64 form
         if (a.fb == 32 && a.lc == 3 && a.lp == 0 && a.pb == 2 && a.eos == 0) {
             launch_spec<PairT, LIT, PBS, 1>(ctx, a, grid, lds, st);
             return;
@@ -1883,21 +1841,9 @@ static void launch_pb(Ctx* ctx, const EncArgs& a, int grid, size_t lds, hipStrea
     else launch_one<PairT, LIT, 4>(ctx, a, grid, lds, st);
 }
 
-// The two-wave parse for launches with few streams per CU (a single long stream, strong
-// scaling's share of a buffer; up to 4 per CU: 2 waves per SIMD at 256 VGPRs). Measured on
-// MI355X it runs as fast as the one-wave parse and no faster (DESIGN.md section 5, round 4:
-// R is the small part of a position; S and N, the chain, stay serial), so it is off unless
-// LZG_ENC_W2=1 (the CPU emulation test runs both forms).
-static bool want_w2(const EncArgs& a, int grid) {
-    if (a.fb > 32) return false;   // the ring (SPEC 1 / 2) only
-    static const int force = exp_env("LZG_ENC_W2") ? atoi(exp_env("LZG_ENC_W2")) : -1;
-    return force > 0 && grid <= kFewStreams;
-}
-
 int launch_encoder(Ctx* ctx, const EncArgs& a0, bool wide_pairs, int grid, hipStream_t st) {
     if (a0.pair_bytes != (wide_pairs ? 8u : 4u)) return ctx->fail(LZMA_E_INTERNAL, "pair width mismatch");
     EncArgs a = a0;
-    a.w2 = want_w2(a, grid) ? 1u : 0u;
     size_t lds = enc_lds_bytes(a);
     if (lds > 160 * 1024) return ctx->fail(LZMA_E_PARAM, "encoder LDS %zu too large", lds);
     if (wide_pairs) {

@@ -79,11 +79,11 @@ struct ProbLayout {
     static constexpr int RLEN = LEN + LSIZE;
     static constexpr int COUNT = RLEN + LSIZE;
 };
-__host__ __device__ inline uint32_t prob_count(uint32_t pb) {
+__host__ __device__ constexpr uint32_t prob_count(uint32_t pb) {
     return pb <= 2 ? (uint32_t)ProbLayout<2>::COUNT : (uint32_t)ProbLayout<4>::COUNT;
 }
 // the decision models (isMatch, isRep, isRepG0-2, isRep0Long) are the first PSLOT entries
-__host__ __device__ inline uint32_t dm_count(uint32_t pb) {
+__host__ __device__ constexpr uint32_t dm_count(uint32_t pb) {
     return pb <= 2 ? (uint32_t)ProbLayout<2>::PSLOT : (uint32_t)ProbLayout<4>::PSLOT;
 }
 

@@ -340,7 +340,6 @@ struct EncArgs {
     uint32_t fb, lc, lp, pb, eos, dist_table_size, len_table_size;
     uint32_t lit_in_lds;
     uint32_t pair_bytes;          // 4 (u32 packed pairs) or 8 (u64, streams >= 8 MiB)
-    uint32_t w2;                  // two waves per stream (enc.hip W2: few streams per CU); set by launch_encoder
     uint32_t* dbg;                // debug checkpoints (host-mapped, LZMA_MI355X_DEBUG only) or null
     uint64_t* prof;               // phase cycles [nstreams][kProfSlots] (LZG_PROF builds) or null
 };

@@ -34,6 +34,7 @@ def test_bench_gpus2_launcher_emulated(tmp_path):
     assert len(lines) == 1, out.stdout[-3000:]   # ONE JSON line, from rank 0
     res = json.loads(lines[0])
     assert res["n_gpus"] == 2 and res["scaling"] == "strong" and res["verified"]
+    assert res["sequential"]["lengths_equal_timed_steps"] and res["parse_fence"] is False
     n_all = (size + chunk - 1) // chunk
     assert res["config"]["streams_per_gpu"] == n_all // 2
     g = res["gathered"]

@@ -13,19 +13,16 @@ SIMT = os.path.join(REPO, "tests", "simt")
 
 
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize("form", ["default", "bench_form", "two_wave"])
+@pytest.mark.parametrize("form", ["default", "bench_form"])
 def test_emulated_kernels_bit_exact_under_asan(form):
     """form: the parser as these small batches run it by default (one wave per stream, the
     literal coders in LDS: few streams per CU); as the 4096-stream bench runs it (literal
-    coders in HBM, LZG_ENC_LITLDS=0); and the two-wave parse (enc.hip W2, LZG_ENC_W2=1).
-    The last two on the smaller input set ("tiny")."""
+    coders in HBM, LZG_ENC_LITLDS=0), on the smaller input set ("tiny")."""
     subprocess.check_call(["make", "-s", "-j", "8", "-C", SIMT])
     env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0", UBSAN_OPTIONS="print_stacktrace=1")
     mode = "quick"
     if form == "bench_form":
         env["LZG_ENC_LITLDS"], mode = "0", "tiny"
-    elif form == "two_wave":
-        env["LZG_ENC_W2"], mode = "1", "tiny"
     r = subprocess.run([os.path.join(SIMT, "build", "emu_check"), mode], capture_output=True, text=True,
                        env=env, timeout=600)
     tail = "\n".join((r.stdout + r.stderr).splitlines()[-20:])
