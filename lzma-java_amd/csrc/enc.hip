@@ -61,20 +61,6 @@ constexpr uint32_t kPosMask = 0xFFFu, kPos2Shift = 12, kFlagShift = 24;
 static_assert(kNumOpts <= 4096, "PosPrev fits 12 bits");
 
 #define FI __device__ __forceinline__
-// Parse-kernel variants under A/B measurement (0 = off in the product build; `make exp` style
-// builds set them with -D): see DESIGN.md section 5, round 5.
-#ifndef LZG_EXP_BRANCHFREE_STATE
-#define LZG_EXP_BRANCHFREE_STATE 0
-#endif
-#ifndef LZG_EXP_PARK
-#define LZG_EXP_PARK 0
-#endif
-#ifndef LZG_EXP_LITPF
-#define LZG_EXP_LITPF 0
-#endif
-#ifndef LZG_EXP_STATIC_LDS
-#define LZG_EXP_STATIC_LDS 1   // measured: one stream -9 %, 512 streams -10 %, 4096 flat (round 5)
-#endif
 // Lanes of one wavefront exchange data through LDS. The hardware runs one
 // wave's LDS instructions in order; this compiler barrier keeps the IR and
 // machine schedulers from moving LDS accesses across an exchange point.
@@ -217,12 +203,9 @@ struct Enc {
     // ---- RING bookkeeping of _optimum (see the accessors)
     uint32_t ring_top;        // highest slot whose ahead fields are in the ring
     uint32_t far_valid;       // slot cur + 65 is held in the far entry (kFarEntry)
-    // The coder's state, parked in LDS while getOptimum's forward loop runs (park / unpark):
-    // none of it is read there, so none of it holds a register there (the kernel is at its
-    // SGPR limit). FairPrio's state lives only here.
+    // State that no loop reads, kept in LDS instead of registers (the kernel is at its SGPR
+    // limit): FairPrio's (read once per 1/256 of the stream)
     struct Cold {
-        uint64_t recs, rcap, rpos;
-        uint32_t rd0, rd1, rd2, rd3, state, prev_byte, mpc, apc, overflow, dts;
         FairPrio prio;
     };
     Cold* cold;
@@ -237,14 +220,6 @@ struct Enc {
     static constexpr int kMO = RING ? 0 : 1;     // the bit of offset 0
     GM gm0, gm1, gm2, gm3, gmp0, gmp1;
     uint32_t g_prev, g_cur, g_mb;   // bytes at p - 1 and p, and at p - rep0 - 1 (the match byte), from the gather
-    uint32_t g_next;                // byte at p + 1 (the next position's literal), from the gather
-#if LZG_EXP_LITPF
-    // The next forward position's literal probabilities, loaded one position ahead (its coder
-    // and symbol are input bytes, known before its state is): bit slot j's three candidates
-    // (normal, matched with match bit 0, matched with match bit 1). The literal coders do not
-    // change within a forward pass (only the coder, between passes, adapts them).
-    uint32_t lpf0[kLitSlots], lpf1[kLitSlots], lpf2[kLitSlots];
-#endif
 #ifdef LZG_PROF
     uint64_t prof[kProfSlots];
 #endif
@@ -406,55 +381,6 @@ struct Enc {
         return (uint32_t)__builtin_amdgcn_readfirstlane((int)price);
 #endif
     }
-#if LZG_EXP_LITPF
-    // issue the loads of position `pos`'s literal probabilities (coder after byte `prev`, symbol `sym`)
-    FI void lit_prefetch(uint32_t pos, uint32_t prev, uint32_t sym) {
-        const uint16_t* p = lit_coder(pos, prev);
-#pragma unroll
-        for (int t = 0; t < kLitSlots; t++) {
-#if LZG_WAVE == 64
-            const int i = 7 - (int)(lane & 7u);   // lanes 8-63 repeat lanes 0-7
-#else
-            const int i = 7 - (t * kWave + (int)lane);
-#endif
-            const uint32_t ctx = (0x100u | sym) >> (i + 1);
-            lpf0[t] = p[ctx]; lpf1[t] = p[0x100u + ctx]; lpf2[t] = p[0x200u + ctx];
-        }
-    }
-    // lit_price of the prefetched position (the same symbol): selects, no memory round trip
-    FI uint32_t lit_price_pf(bool match_mode, uint32_t mb, uint32_t sym) const {
-        int first = -1;
-        if (match_mode) {
-            uint32_t diff = (mb ^ sym) & 0xFFu;
-            first = diff ? 31 - __clz(diff) : -1;
-        }
-        uint32_t price = 0;
-#pragma unroll
-        for (int t = 0; t < kLitSlots; t++) {
-#if LZG_WAVE == 64
-            const int i = 7 - (int)(lane & 7u);
-#else
-            const int i = 7 - (t * kWave + (int)lane);
-#endif
-            const uint32_t bit = (sym >> i) & 1;
-            const uint32_t v = (match_mode && i >= first) ? (((mb >> i) & 1u) ? lpf2[t] : lpf1[t]) : lpf0[t];
-            const uint32_t pr = price_bit(v, bit);
-#if LZG_WAVE == 64
-            price = lane < 8 ? pr : 0u;
-#else
-            price += pr;
-#endif
-        }
-#if LZG_WAVE == 64
-        price += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)price, 0xB1, 0xF, 0xF, false);
-        price += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)price, 0x4E, 0xF, 0xF, false);
-        price += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)price, 0x12C, 0xF, 0xF, false);
-        return (uint32_t)__builtin_amdgcn_readlane((int)price, 0);
-#else
-        return (uint32_t)__builtin_amdgcn_readfirstlane((int)price);
-#endif
-    }
-#endif
     FI uint32_t len_price(int which, uint32_t sym, uint32_t ps) const {
         return lenp[(which << pb) * tsize + ps * tsize + sym];
     }
@@ -525,7 +451,6 @@ struct Enc {
         g_prev = lane_value(va, 0);
         g_cur = lane_value(va, 1);
         g_mb = lane_value(v0, 1);
-        g_next = lane_value(va, 2);
         LANE_FENCE();
     }
     // byte at p + o on the cur side
@@ -1113,9 +1038,6 @@ struct Enc {
         PBEGIN(t1);
         uint32_t p1 = dm0(E_IS_MATCH + (state << PBS) + pos_state) +
                       lit_price(lit_coder(position, g_prev), !st_is_char(state), match_byte, cur_byte);
-#if LZG_EXP_LITPF
-        lit_prefetch(position + 1, cur_byte, g_next);   // the forward loop's first position
-#endif
         PEND(PF_LIT, t1);
         uint32_t match_price = dm1(E_IS_MATCH + (state << PBS) + pos_state);
         uint32_t rep_match_price = match_price + dm1(E_IS_REP + state);
@@ -1175,36 +1097,6 @@ struct Enc {
         // the predecessor may be in HBM (a path back by 65), checked per access.
         constexpr bool FA = F || RING, FB = F;
         PosS r;
-#if LZG_EXP_BRANCHFREE_STATE
-        // slot cur's link (Encoder.java:518-535): one LDS round trip, then scalars
-        const uint32_t ppc = uni32(pp_at<FA>(cur));
-        const int32_t bpc = (int32_t)uni32((uint32_t)bp_at<FA>(cur));
-        const uint32_t fsc = ppc >> kFlagShift;
-        const bool c1 = (fsc & 1u) != 0, c2 = (fsc & 3u) == 3u;   // Prev1IsChar; Prev1IsChar && Prev2
-        // BackPrev2, meaningful with Prev2 only: read beside the others in LDS, on demand from HBM
-        const int32_t bp2c = FA ? (int32_t)uni32((uint32_t)bp2_at<FA>(cur)) : (c2 ? bp2_at<FA>(cur) : 0);
-        const uint32_t pp2 = (ppc >> kPos2Shift) & kPosMask;
-        const uint32_t pprev = (ppc & kPosMask) - (c1 ? 1u : 0u);
-        const bool lit_path = pprev == cur - 1;   // a literal or short rep from cur - 1: reps unchanged
-        // the slot both the start state and the Backs come from (PosPrev2 on a Prev2 path)
-        const uint32_t q = c2 ? pp2 : pprev;
-        const uint32_t sw = uni32(bytes_at<FB>(q, cur - 1));   // its byte record | State << 24
-        const v4u32 b = backs4_at<FB>(q, cur - 1);
-        // the state, branch-free (Encoder.java:520-555)
-        uint32_t st = sw >> 24;
-        st = c2 ? (bp2c < kNumRepDistances ? st_long(st) : st_match(st)) : st;
-        st = c1 ? st_lit(st) : st;
-        const int32_t pos = c2 ? bp2c : bpc;   // the last symbol's back on a non-literal path
-        st = lit_path ? (bpc == 0 ? st_short(st) : st_lit(st)) : ((c2 || pos < kNumRepDistances) ? st_long(st) : st_match(st));
-        // the reps (Encoder.java:556-584): a rep r moves Backs[r] to the front, a match
-        // shifts its distance in (the rep-3 pattern for reps 1..3)
-        const uint32_t b0 = uni32(b[0]), b1 = uni32(b[1]), b2 = uni32(b[2]), b3 = uni32(b[3]);
-        const int32_t r3 = pos < kNumRepDistances ? pos : 3;
-        const uint32_t n0 = pos < kNumRepDistances ? (pos == 0 ? b0 : (pos == 1 ? b1 : (pos == 2 ? b2 : b3)))
-                                                   : (uint32_t)(pos - kNumRepDistances);
-        const uint32_t n1 = r3 == 0 ? b1 : b0, n2 = r3 <= 1 ? b2 : b1, n3 = r3 <= 2 ? b3 : b2;
-        if (!lit_path) { rp0 = n0; rp1 = n1; rp2 = n2; rp3 = n3; }
-#else
         uint32_t st;
         uint32_t ppc = pp_at<FA>(cur);
         uint32_t pos_prev_c = ppc & kPosMask;
@@ -1245,7 +1137,6 @@ struct Enc {
                 rp0 = (uint32_t)(pos - kNumRepDistances); rp1 = b0; rp2 = b1; rp3 = b2;
             }
         }
-#endif
         if (RING) {   // cur's entry held cur - 64
             if (!F && cur >= (uint32_t)kOptLds) evict_behind(cur - (uint32_t)kOptLds);
         }
@@ -1266,14 +1157,8 @@ struct Enc {
         r.cur_byte = g_cur;
         r.match_byte = g_mb;
         PBEGIN(tl);
-#if LZG_EXP_LITPF
-        r.cur_and1 = r.cur_price + dm0(E_IS_MATCH + (r.st << PBS) + r.pos_state) +
-                     lit_price_pf(!st_is_char(r.st), r.match_byte, r.cur_byte);
-        lit_prefetch(position + 1, r.cur_byte, g_next);   // for cur + 1, under this step's relaxations
-#else
         r.cur_and1 = r.cur_price + dm0(E_IS_MATCH + (r.st << PBS) + r.pos_state) +
                      lit_price(lit_coder(position, g_prev), !st_is_char(r.st), r.match_byte, r.cur_byte);
-#endif
         PEND(PF_LIT, tl);
     }
     // N: slot cur + 1's literal and short-rep candidates (nx_*: its fields, read by the caller)
@@ -1459,34 +1344,7 @@ struct Enc {
         }
     }
 
-    FI void park() {
-        Cold* c = cold;
-        c->recs = (uint64_t)recs; c->rcap = rcap; c->rpos = rpos;
-        c->rd0 = rd0; c->rd1 = rd1; c->rd2 = rd2; c->rd3 = rd3;
-        c->state = state; c->prev_byte = prev_byte; c->mpc = match_price_count; c->apc = align_price_count;
-        c->overflow = overflow; c->dts = dist_table_size;
-        LANE_FENCE();   // a compiler memory barrier: unpark's loads are not forwarded from these stores
-    }
-    FI void unpark() {
-        LANE_FENCE();
-        const Cold* c = cold;
-        recs = (uint16_t*)uni64(c->recs); rcap = uni64(c->rcap); rpos = uni64(c->rpos);
-        rd0 = uni32(c->rd0); rd1 = uni32(c->rd1); rd2 = uni32(c->rd2); rd3 = uni32(c->rd3);
-        state = uni32(c->state); prev_byte = uni32(c->prev_byte);
-        match_price_count = uni32(c->mpc); align_price_count = uni32(c->apc);
-        overflow = uni32(c->overflow); dist_table_size = uni32(c->dts);
-    }
     FI uint32_t parse_forward(uint32_t position, int32_t* back_res, uint32_t len_end) {
-#if LZG_EXP_PARK
-        park();
-        const uint32_t len = parse_forward_loop(position, back_res, len_end);
-        unpark();
-        return len;
-#else
-        return parse_forward_loop(position, back_res, len_end);
-#endif
-    }
-    FI uint32_t parse_forward_loop(uint32_t position, int32_t* back_res, uint32_t len_end) {
         uint32_t cur = 0;
         DBG(5, len_end);
         for (;;) {
@@ -1697,12 +1555,10 @@ template <typename PairT, bool LIT_LDS, int PBS, int SPEC>
 __global__ void __launch_bounds__(kWave, 4) enc_kernel(EncArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint8_t* sm = smem;
-#if LZG_EXP_STATIC_LDS
     // SPEC 1: a static array, so every LDS offset folds into its ds instruction (other
     // kernels: a 16-byte placeholder, the dynamic array is theirs)
     __shared__ __attribute__((aligned(16))) uint8_t smem_s[SPEC == 1 ? kSpec1LdsBytes<(int)sizeof(PairT), LIT_LDS> : 16u];
-    if constexpr (SPEC == 1) sm = smem_s;
-#endif
+    if constexpr (SPEC == 1) sm = smem_s;   // measured: one stream -9 %, 512 streams -10 %, 4096 flat (round 5)
     Enc<PairT, LIT_LDS, PBS, (SPEC != 0)> e;   // SPEC 1 and 2: fb <= 32, the _optimum ring
     e.lane = threadIdx.x % kWave;
     if (SPEC == 1) {
@@ -1817,7 +1673,7 @@ int enc_grid(const Derived&, int nstreams) { return nstreams; }   // one workgro
 template <typename PairT, bool LIT, int PBS, int SPEC>
 static void launch_spec(Ctx* ctx, const EncArgs& a, int grid, size_t lds, hipStream_t st) {
     TimedLaunch tl(ctx, "enc_parse", st);
-    if (LZG_EXP_STATIC_LDS && SPEC == 1) lds = 0;   // the kernel's static array
+    if (SPEC == 1) lds = 0;   // the kernel's static array
     if (lds > 64 * 1024)
         hipFuncSetAttribute((const void*)enc_kernel<PairT, LIT, PBS, SPEC>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL((enc_kernel<PairT, LIT, PBS, SPEC>), dim3(grid), dim3(kWave), lds, st, a);
@@ -1846,6 +1702,12 @@ int launch_encoder(Ctx* ctx, const EncArgs& a0, bool wide_pairs, int grid, hipSt
     EncArgs a = a0;
     size_t lds = enc_lds_bytes(a);
     if (lds > 160 * 1024) return ctx->fail(LZMA_E_PARAM, "encoder LDS %zu too large", lds);
+#ifdef LZG_ONLY_SPEC1_LIT   // code-inspection builds (assembly of one kernel family)
+    if (!wide_pairs) {
+        if (a.lit_in_lds) launch_spec<uint32_t, true, 2, 1>(ctx, a, grid, lds, st);
+        else launch_spec<uint32_t, false, 2, 1>(ctx, a, grid, lds, st);
+    }
+#else
     if (wide_pairs) {
         if (a.lit_in_lds) launch_pb<uint64_t, true>(ctx, a, grid, lds, st);
         else launch_pb<uint64_t, false>(ctx, a, grid, lds, st);
@@ -1853,6 +1715,7 @@ int launch_encoder(Ctx* ctx, const EncArgs& a0, bool wide_pairs, int grid, hipSt
         if (a.lit_in_lds) launch_pb<uint32_t, true>(ctx, a, grid, lds, st);
         else launch_pb<uint32_t, false>(ctx, a, grid, lds, st);
     }
+#endif
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return ctx->fail(LZMA_E_DEVICE, "enc launch: %s", hipGetErrorString(e));
     return LZMA_OK;
