@@ -499,6 +499,30 @@ def test_gpu_config3_text_dict28(ctx):
 
 
 @pytest.mark.timeout(600)
+def test_gpu_config3_text_dict28_two_32mib_streams(ctx, heartbeat):
+    """Config 3's window regime: two TEXT streams of 32 MiB at dict 2^28 (26
+    hash bits, distTableSize 56), L5 -- streams far past the bench's 256 KiB chunks, so
+    matches and reps reach back tens of MiB, and past 8 MiB (64-bit pairs, the bench-parameter
+    parse kernel in its wide form). Byte-equal to Encoder.Code (the oracle, on two host
+    threads beside the GPU encode), and decoded back."""
+    import concurrent.futures as cf
+    chunk = 32 << 20
+    data = lzma_amd.text_generate(2 * chunk)
+    streams = [data[:chunk].tobytes(), data[chunk:].tobytes()]
+    p = lzma_amd.make_params(dict_size=1 << 28, fb=32, mf=1)
+    ctx.set_batch_bytes(1 << 30)
+    with cf.ThreadPoolExecutor(2) as ex:
+        futs = [ex.submit(lambda s=s: orc.EncoderSession(_oparams(p)).encode(s)) for s in streams]
+        outs = ctx.encode_batch(streams, p)
+        refs = [f.result() for f in futs]
+    for i, (o, r) in enumerate(zip(outs, refs)):
+        assert len(o) == len(r) and o == r, "stream %d" % i
+    dec = ctx.decode_batch(outs, lzma_amd.write_props(p), [chunk] * 2)
+    for s, (st, d) in zip(streams, dec):
+        assert st == lzma_amd.LZMA_OK and d == s
+
+
+@pytest.mark.timeout(600)
 def test_gpu_config3_full_1gib_text_dict28_every_stream(ctx, heartbeat):
     """Config 3 at its full size: 1 GiB of TEXT ("enwik9-shaped") data as 4096
     independent 256 KiB streams (the bench's --data text chunking) at dict 2^28 L5,
