@@ -522,13 +522,13 @@ _KERNEL_OF = {"enc_parse": "enc_kernel", "dec_stream": "dec_kernel", "mf_walk": 
 
 
 def _profile_prefix(wl):
-    """config 3 (TEXT) has its own summaries (round 3, tools/r03_text.sh); the bench
-    workload's are round 4's (tools/r04/prof.sh)"""
-    return "r03/text_" if wl.get("data") == "text" else "r04/"
+    """round 5's summaries (tools/r05/prof.sh, DATA=bench / DATA=text) of this same
+    workload, taken at the kernels this tree builds"""
+    return "r05/text_" if wl.get("data") == "text" else "r05/"
 
 
 def _profile(name, wl):
-    """A committed per-kernel summary from profiles/ (written by tools/r04/prof.sh
+    """A committed per-kernel summary from profiles/ (written by tools/r05/prof.sh
     over this same workload), or None when absent or taken on another workload."""
     path = os.path.join(REPO, "profiles", _profile_prefix(wl) + name)
     if not os.path.exists(path):

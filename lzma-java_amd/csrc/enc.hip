@@ -70,11 +70,11 @@ static_assert(kNumOpts <= 4096, "PosPrev fits 12 bits");
 // loop itself stays a scalar loop (a lane-dependent exit costs exec-mask
 // bookkeeping on every iteration and makes values after it look per-lane).
 #define LANE_FOR(T, v, lo, hi) \
-    for (T v##_0 = (lo); v##_0 < (hi); v##_0 += kWave) if (const T v = v##_0 + (T)lane; v < (hi))
+    for (T v##_0 = (lo); v##_0 < (hi); v##_0 += kWave) if (const T v = v##_0 + (T)lane_id(); v < (hi))
 // debug checkpoint (block 0, lane 0) into host-mapped memory
 // (LZG_DEBUG builds only)
 #ifdef LZG_DEBUG
-#define DBG(k, v) do { if (dbg && blockIdx.x == 0 && lane == 0) __hip_atomic_store(dbg + (k), (uint32_t)(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); } while (0)
+#define DBG(k, v) do { if (dbg && blockIdx.x == 0 && lane_id() == 0) __hip_atomic_store(dbg + (k), (uint32_t)(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); } while (0)
 #else
 #define DBG(k, v) do {} while (0)
 #endif
@@ -149,7 +149,21 @@ struct Enc {
                          E_G2 = PL::G2, E_R0L = PL::R0L, E_PSLOT = PL::PSLOT, E_PENC = PL::PENC,
                          E_ALIGN = PL::ALIGN, E_LEN = PL::LEN, E_RLEN = PL::RLEN, E_LOW = PL::LOW,
                          E_MID = PL::MID, E_HIGH = PL::HIGH, E_COUNT = PL::COUNT;
-    uint32_t lane;
+    uint32_t lane_v;          // threadIdx.x: read through lane_id()
+    // The lane index. In the kernels whose literal coders live in HBM (many streams per CU:
+    // 16 per CU, a 128-VGPR budget) it is opaque to the optimizer at every use: otherwise LICM
+    // hoists every lane-derived value (lane + c, lane == c, 7 - (lane & 7), ...) of the whole
+    // kernel to its entry, where hundreds of them hold VGPRs and SGPR pairs for the kernel's
+    // lifetime and spilled to scratch (128 VGPRs + scratch -> 56 VGPRs, none; 4096 streams
+    // 569 -> 537 ms). With the literal coders in LDS (few streams per CU, the budget the LDS
+    // leaves is larger) the hoisted values fit, and recomputing them cost one stream 5 %.
+    FI uint32_t lane_id() const {
+        uint32_t l = lane_v;
+#if LZG_WAVE == 64
+        if constexpr (!LIT_LDS) asm volatile("" : "+v"(l));
+#endif
+        return l;
+    }
     // ---- LDS
     uint16_t* pp;             // ProbPrices [512]
     uint16_t* probs;          // fixed models (lzma_common.h layout)
@@ -352,12 +366,12 @@ struct Enc {
 #if LZG_WAVE == 64
         {   // every lane computes bit (lane & 7): no exec-mask bookkeeping on the scalar unit;
             // lanes 8-63 repeat lanes 0-7's addresses and their prices are dropped
-            const int i = 7 - (int)(lane & 7u);
+            const int i = 7 - (int)(lane_id() & 7u);
             const uint32_t bit = (sym >> i) & 1;
             const uint32_t ctx = (0x100u | sym) >> (i + 1);
             const uint32_t idx = (match_mode && i >= first) ? ((1 + ((mb >> i) & 1)) << 8) + ctx : ctx;
             const uint32_t pr = price_bit(p[idx], bit);
-            price = lane < 8 ? pr : 0u;
+            price = lane_id() < 8 ? pr : 0u;
         }
 #else
         LANE_FOR(int, j, 0, 8) {
@@ -395,7 +409,7 @@ struct Enc {
         if (limit <= 0) return 0;
         const uint32_t a = (uint32_t)p0, b = (uint32_t)p0 - (distance + 1);
         for (int32_t i0 = 0; i0 < limit; i0 += kWave) {
-            int32_t i = i0 + (int32_t)lane;
+            int32_t i = i0 + (int32_t)lane_id();
             bool ne = i < limit ? (in_byte(a + (uint32_t)i) != in_byte(b + (uint32_t)i)) : true;
             uint64_t m = wballot(ne);
             if (m) {
@@ -422,7 +436,7 @@ struct Enc {
         uint32_t va[kGI], v0[kGI], v1[kGI], v2[kGI], v3[kGI], w0[kGI], w1[kGI];
 #pragma unroll
         for (int it = 0; it < kGI; it++) {
-            const uint32_t q = gp - 1 + (uint32_t)(it * kWave) + lane;
+            const uint32_t q = gp - 1 + (uint32_t)(it * kWave) + lane_id();
             va[it] = in_byte(q);
             v0[it] = in_byte(q - d0); v1[it] = in_byte(q - d1); v2[it] = in_byte(q - d2); v3[it] = in_byte(q - d3);
             if (with_pairs) { w0[it] = in_byte(q - e0); w1[it] = in_byte(q - e1); }
@@ -431,7 +445,7 @@ struct Enc {
 #pragma unroll
         for (int it = 0; it < kGI; it++) {
             const int sh = it * kWave;
-            const uint32_t k = (uint32_t)sh + lane;
+            const uint32_t k = (uint32_t)sh + lane_id();
             m0 |= (uint64_t)wballot(va[it] == v0[it]) << sh;
             m1 |= (uint64_t)wballot(va[it] == v1[it]) << sh;
             m2 |= (uint64_t)wballot(va[it] == v2[it]) << sh;
@@ -535,7 +549,7 @@ struct Enc {
     FI void q_bit(Q& q, uint32_t index, uint32_t bit) const {
 #pragma unroll
         for (int t = 0; t < kQS; t++) {   // selects, not a branch: the exec-mask juggling runs on the scalar unit
-            const bool m = (uint32_t)(t * kWave) + lane == q.n;
+            const bool m = (uint32_t)(t * kWave) + lane_id() == q.n;
             q.idx[t] = m ? index : q.idx[t];
             q.bit[t] = m ? bit : q.bit[t];
             q.kind[t] = m ? (uint32_t)QK_PROB : q.kind[t];
@@ -546,7 +560,7 @@ struct Enc {
     FI void q_bt(Q& q, uint32_t base, uint32_t nbits, uint32_t sym) const {
 #pragma unroll
         for (int t = 0; t < kQS; t++) {
-            const uint32_t i = (uint32_t)(t * kWave) + lane - q.n;
+            const uint32_t i = (uint32_t)(t * kWave) + lane_id() - q.n;
             const bool m = i < nbits;
             const uint32_t ic = m ? i : 0u;
             q.idx[t] = m ? base + ((sym | (1u << nbits)) >> (nbits - ic)) : q.idx[t];
@@ -560,7 +574,7 @@ struct Enc {
     FI void q_rev(Q& q, uint32_t base, uint32_t nbits, uint32_t sym) const {
 #pragma unroll
         for (int t = 0; t < kQS; t++) {
-            const uint32_t i = (uint32_t)(t * kWave) + lane - q.n;
+            const uint32_t i = (uint32_t)(t * kWave) + lane_id() - q.n;
             const bool in = i < nbits;
             const uint32_t ic = in ? i : 0u;
             const uint32_t m = (1u << ic) | (ic ? brev32(sym) >> (32 - ic) : 0u);
@@ -574,7 +588,7 @@ struct Enc {
     FI void q_direct(Q& q, uint32_t v, uint32_t nbits) const {
 #pragma unroll
         for (int t = 0; t < kQS; t++) {
-            const uint32_t i = (uint32_t)(t * kWave) + lane - q.n;
+            const uint32_t i = (uint32_t)(t * kWave) + lane_id() - q.n;
             const bool m = i < nbits;
             q.bit[t] = m ? (v >> (nbits - 1 - (m ? i : 0u))) & 1u : q.bit[t];
             q.kind[t] = m ? (uint32_t)QK_DIRECT : q.kind[t];
@@ -591,7 +605,7 @@ struct Enc {
         }
 #pragma unroll
         for (int t = 0; t < kQS; t++) {
-            const uint32_t j = (uint32_t)(t * kWave) + lane - q.n;
+            const uint32_t j = (uint32_t)(t * kWave) + lane_id() - q.n;
             const bool m = j < 8u;
             const int i = 7 - (int)(j & 7u);
             const uint32_t ctx = (0x100u | sym) >> (i + 1);
@@ -630,7 +644,7 @@ struct Enc {
         const uint32_t base = (uint32_t)rpos;
 #pragma unroll
         for (int t = 0; t < kQS; t++) {
-            const uint32_t j = (uint32_t)(t * kWave) + lane;
+            const uint32_t j = (uint32_t)(t * kWave) + lane_id();
             const bool isl = q.kind[t] == QK_LIT, isp = q.kind[t] == QK_PROB;
             rbuf[j < q.n ? (base + j) & (kRbuf - 1) : (uint32_t)kRbuf] =
                 (uint16_t)((q.kind[t] == QK_DIRECT ? 0u : pr[t]) | (q.bit[t] << 11));
@@ -789,7 +803,7 @@ struct Enc {
                 }
             } else {
                 for (uint32_t i0 = len_end + 1; i0 <= hi; i0 += kWave) {
-                    const uint32_t i = i0 + lane;
+                    const uint32_t i = i0 + lane_id();
                     o_price[i <= hi ? i : (uint32_t)kOptLds] = kInfinityPrice;
                 }
             }
@@ -800,7 +814,7 @@ struct Enc {
         }
         if (target < (uint32_t)kOptLds) {   // branch-free: idle lanes write the sink slot
             for (uint32_t i0 = len_end + 1; i0 <= target; i0 += kWave) {
-                const uint32_t i = i0 + lane;
+                const uint32_t i = i0 + lane_id();
                 o_price[i <= target ? i : (uint32_t)kOptLds] = kInfinityPrice;
             }
             len_end = target;
@@ -817,7 +831,7 @@ struct Enc {
         if (RING || base_slot + hi < (uint32_t)kOptLds) {   // all slots in LDS: no per-lane spill branches
             // branch-free: idle lanes and lanes that do not improve write the sink slot
             for (uint32_t l0 = lo; l0 <= hi; l0 += kWave) {
-                const uint32_t l = l0 + lane;
+                const uint32_t l = l0 + lane_id();
                 const bool ok = l <= hi;
                 const uint32_t s = ok ? ix(base_slot + l) : (uint32_t)kOptLds;
                 const uint32_t cl = price_base + len_price(1, ok ? l - 2 : 0u, ps);
@@ -845,7 +859,7 @@ struct Enc {
                         uint32_t pos_prev_v) {
         if (RING || base_slot + hi < (uint32_t)kOptLds) {   // all slots in LDS; branch-free as relax_rep
             for (uint32_t l0 = lo; l0 <= hi; l0 += kWave) {
-                const uint32_t l = l0 + lane;
+                const uint32_t l = l0 + lane_id();
                 const bool ok = l <= hi;
                 const uint32_t s = ok ? ix(base_slot + l) : (uint32_t)kOptLds;
                 const uint32_t cl = price_base + pos_len_price(dist, ok ? l : (uint32_t)kMatchMinLen, ps);
@@ -873,7 +887,7 @@ struct Enc {
     FI void relax_first(uint32_t lstart, uint32_t len_main, uint32_t npairs, uint32_t normal_match_price, uint32_t pos_state) {
         if (F) {   // all slots in LDS: branch-free (idle and non-improving lanes write the sink slot)
             for (uint32_t l0 = lstart; l0 <= len_main; l0 += kWave) {
-                const uint32_t l = l0 + lane;
+                const uint32_t l = l0 + lane_id();
                 const bool ok = l <= len_main;
                 // the pair of length l: the first with md_len >= l (lengths increase), i.e. the count of
                 // shorter ones among the first npairs - 1 -- a uniform loop instead of a per-lane while
@@ -1470,7 +1484,7 @@ struct Enc {
         DBG(1, 4);
 
         uint32_t now_pos = 0;
-        cold->prio.start(g_enc_sched, n, lane);
+        cold->prio.start(g_enc_sched, n, lane_id());
         if (avail() == 0) { flush(0); return; }
         read_match_distances();
         DBG(1, 5);
@@ -1517,7 +1531,7 @@ struct Enc {
                 if (match_price_count >= (1u << 7)) fill_distances_prices();
                 if (align_price_count >= (uint32_t)kAlignTableSize) fill_align_prices();
                 PEND(PF_TABLES, tt);
-                cold->prio.update(now_pos, lane);
+                cold->prio.update(now_pos, lane_id());
                 if (avail() == 0) { flush(now_pos); return; }
             }
         }
@@ -1560,7 +1574,7 @@ __global__ void __launch_bounds__(kWave, 4) enc_kernel(EncArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t smem_s[SPEC == 1 ? kSpec1LdsBytes<(int)sizeof(PairT), LIT_LDS> : 16u];
     if constexpr (SPEC == 1) sm = smem_s;   // measured: one stream -9 %, 512 streams -10 %, 4096 flat (round 5)
     Enc<PairT, LIT_LDS, PBS, (SPEC != 0)> e;   // SPEC 1 and 2: fb <= 32, the _optimum ring
-    e.lane = threadIdx.x % kWave;
+    e.lane_v = threadIdx.x % kWave;
     if (SPEC == 1) {
         e.fb = 32; e.lc = 3; e.lp = 0; e.pb = 2; e.ps_mask = 3; e.eos = 0; e.tsize = 31;
     } else {
@@ -1601,11 +1615,11 @@ __global__ void __launch_bounds__(kWave, 4) enc_kernel(EncArgs a) {
     uint16_t* lit_g = (uint16_t*)(a.lit_scratch + (size_t)blockIdx.x * a.lit_stride);
     if (LIT_LDS) e.lit = (uint16_t*)(sm + off[L_LIT]);
     else e.lit = lit_g;
-    for (int i0 = 0; i0 < 512; i0 += kWave) e.pp[i0 + e.lane] = (uint16_t)c_tab.prices[i0 + e.lane];
+    for (int i0 = 0; i0 < 512; i0 += kWave) e.pp[i0 + e.lane_v] = (uint16_t)c_tab.prices[i0 + e.lane_v];
     LANE_FENCE();
     e.dbg = a.dbg;
 #ifdef LZG_DEBUG
-    if (e.dbg && blockIdx.x == 0 && e.lane == 0) __hip_atomic_store(e.dbg, 7u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (e.dbg && blockIdx.x == 0 && e.lane_v == 0) __hip_atomic_store(e.dbg, 7u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 #endif
     e.pairs = a.pairs;
     e.ovf_off = a.ovf_off;
@@ -1618,7 +1632,7 @@ __global__ void __launch_bounds__(kWave, 4) enc_kernel(EncArgs a) {
     const int s = __builtin_amdgcn_readfirstlane((int)a.order[blockIdx.x]);
     if (s < 0 || s >= a.nstreams) return;   // a corrupt order entry: touch nothing (the host checked the order it wrote)
     if (uni64(a.offs[s + 1]) < uni64(a.offs[s]) || uni64(a.rec_offs[s + 1]) < uni64(a.rec_offs[s])) {
-        if (e.lane == 0) { a.rec_lens[s] = 0; a.out_lens[s] = 9ull << 32; a.status[s] = LZMA_E_INTERNAL; }
+        if (e.lane_v == 0) { a.rec_lens[s] = 0; a.out_lens[s] = 9ull << 32; a.status[s] = LZMA_E_INTERNAL; }
         return;
     }
     e.gbase = uni64(a.offs[s]);
@@ -1629,25 +1643,25 @@ __global__ void __launch_bounds__(kWave, 4) enc_kernel(EncArgs a) {
     e.recs = a.recs + ro;
     e.rcap = uni64(a.rec_offs[s + 1]) - ro;
 #ifdef LZG_DEBUG
-    if (e.dbg && e.lane == 0) __hip_atomic_store(e.dbg + 8, (uint32_t)s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (e.dbg && e.lane_v == 0) __hip_atomic_store(e.dbg + 8, (uint32_t)s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 #endif
 #ifdef LZG_PROF
     const uint64_t t_run = __builtin_amdgcn_s_memtime();
     const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
 #endif
     e.run();
-    e.cold->prio.finish(e.lane);
+    e.cold->prio.finish(e.lane_v);
 #ifdef LZG_PROF
     e.prof[PF_TOTAL] = __builtin_amdgcn_s_memtime() - t_run;
     e.prof[PF_T0] = rt0;   // 100 MHz wall clock: where each stream ran
     e.prof[PF_T1] = __builtin_amdgcn_s_memrealtime();
     // HW_REG_HW_ID (cu / sh / se / simd) and HW_REG_XCC_ID
     e.prof[PF_HWID] = (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 4) | ((uint64_t)__builtin_amdgcn_s_getreg((15 << 11) | 20) << 32);
-    if (e.lane == 0 && a.prof)
+    if (e.lane_v == 0 && a.prof)
         for (int k = 0; k < kProfSlots; k++) a.prof[(size_t)s * kProfSlots + k] = e.prof[k];
 #endif
     if (e.overflow && !e.bad) e.bad = 7;   // record region smaller than rc_record_bound(): a bug, not the data
-    if (e.lane == 0) {
+    if (e.lane_v == 0) {
         a.rec_lens[s] = e.rpos;
         if (e.bad) a.out_lens[s] = ((uint64_t)e.bad << 32) | e.mfpos;
         a.status[s] = e.bad ? LZMA_E_INTERNAL : LZMA_OK;
