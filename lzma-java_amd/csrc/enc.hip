@@ -1103,6 +1103,10 @@ struct Enc {
     // the literal / short-rep update of slot cur + 1, which cur - 1's longer candidates may
     // have written).
     struct PosS { uint32_t st, pos_state, cur_price, cur_and1, cur_byte, match_byte; };
+#ifndef LZG_VSEL_STATE
+#define LZG_VSEL_STATE 2
+#endif
+    static constexpr bool kVselState = LZG_VSEL_STATE == 2 ? true : (LZG_VSEL_STATE == 1 ? !LIT_LDS : false);
     template <bool F>
     FI PosS pos_state_part(uint32_t cur, uint32_t position) {
         PBEGIN(ts);
@@ -1111,6 +1115,55 @@ struct Enc {
         // the predecessor may be in HBM (a path back by 65), checked per access.
         constexpr bool FA = F || RING, FB = F;
         PosS r;
+        if constexpr (F && kVselState) {
+            // Branch-free form (the many-streams kernel, where the vector unit is idle and the
+            // scalar unit is the shared resource): the derivation below as mask arithmetic on the
+            // LDS-loaded values (bit operations the compiler cannot turn back into branches), with
+            // one 16-byte Backs read whether or not it is needed. The State transitions (Base.java
+            // :16-36) as packed 4-bit tables / closed forms: match 7 | 10, long 8 | 11, short 9 | 11.
+            constexpr uint64_t kLitT = 0x54654321'0000ull;   // st_lit: 0 0 0 0 1 2 3 4 5 6 4 5
+            const uint32_t ppc = pp_at<true>(cur);
+            const uint32_t bpc = (uint32_t)bp_at<true>(cur), bp2c = (uint32_t)bp2_at<true>(cur);
+            const uint32_t c1 = (ppc >> kFlagShift) & 1u;                                // Prev1IsChar
+            const uint32_t c2 = (ppc >> (kFlagShift + 1)) & c1;                          // and Prev2
+            const uint32_t m2 = 0u - c2;
+            const uint32_t pp2 = (ppc >> kPos2Shift) & kPosMask;
+            const uint32_t pprev = (ppc & kPosMask) - c1;
+            const uint32_t q = pprev ^ ((pp2 ^ pprev) & m2);   // the slot of the start state and of the Backs
+            const uint32_t mlit = 0u - (uint32_t)(pprev == cur - 1);   // a literal / short rep from cur - 1
+            const uint32_t st0 = state_at<true>(q, cur - 1);
+            const v4u32 b = backs4_at<true>(q, cur - 1);
+            const uint32_t pos = bpc ^ ((bp2c ^ bpc) & m2);   // the last symbol's back (int32 as bits)
+            const uint32_t rep_pos = (uint32_t)((int32_t)pos < kNumRepDistances);
+            // st1: after the Prev2 symbol (long rep or match), st2: after the middle literal
+            const uint32_t a1 = 7u + 3u * (uint32_t)(st0 >= 7u) + (uint32_t)((int32_t)bp2c < kNumRepDistances);
+            const uint32_t st1 = st0 ^ ((a1 ^ st0) & m2);
+            const uint32_t l2 = (uint32_t)(kLitT >> (4u * st1)) & 15u;
+            const uint32_t st2 = st1 ^ ((l2 ^ st1) & (0u - c1));
+            const uint32_t hi2 = (uint32_t)(st2 >= 7u);
+            const uint32_t lit_st = bpc == 0u ? 9u + 2u * hi2 : ((uint32_t)(kLitT >> (4u * st2)) & 15u);
+            const uint32_t far_st = 7u + 3u * hi2 + (c2 | rep_pos);
+            const uint32_t st = far_st ^ ((lit_st ^ far_st) & mlit);
+            // the reps: a rep r moves Backs[r] to the front, a match shifts its distance in
+            const uint32_t r3 = pos < 3u ? pos : 3u;   // (as unsigned: a match, and -1, give 3)
+            const uint32_t b0 = b[0], b1 = b[1], b2 = b[2], b3 = b[3];
+            const uint32_t e0 = 0u - (uint32_t)(r3 == 0u), e1 = 0u - (uint32_t)(r3 == 1u), e2 = 0u - (uint32_t)(r3 == 2u);
+            const uint32_t br = (b0 & e0) | (b1 & e1) | (b2 & e2) | (b3 & ~(e0 | e1 | e2));
+            const uint32_t n0 = rep_pos ? br : pos - (uint32_t)kNumRepDistances;
+            const uint32_t n1 = b0 ^ ((b1 ^ b0) & e0);
+            const uint32_t n2 = b1 ^ ((b2 ^ b1) & (e0 | e1));
+            const uint32_t n3 = b2 ^ ((b3 ^ b2) & ~(0u - (uint32_t)(r3 == 3u)));
+            rp0 = n0 ^ ((rp0 ^ n0) & mlit);
+            rp1 = n1 ^ ((rp1 ^ n1) & mlit);
+            rp2 = n2 ^ ((rp2 ^ n2) & mlit);
+            rp3 = n3 ^ ((rp3 ^ n3) & mlit);
+            set_backs4<true>(cur, rp0, rp1, rp2, rp3);
+            r.cur_price = price_at<true>(cur);
+            r.pos_state = position & ps_mask;
+            r.st = st;
+            PEND(PF_STATE, ts);
+            return r;
+        }
         uint32_t st;
         uint32_t ppc = pp_at<FA>(cur);
         uint32_t pos_prev_c = ppc & kPosMask;

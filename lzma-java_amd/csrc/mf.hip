@@ -96,26 +96,59 @@ __global__ void __launch_bounds__(256) mf_prev_kernel(const uint32_t* __restrict
     prev[vals[i]] = (i > 0 && keys[i - 1] == k) ? vals[i - 1] : kNoPos;
 }
 
+// Unaligned 8-byte little-endian load from a buffer padded by >= 16 bytes.
+__device__ inline uint64_t load8(const uint8_t* p) {
+    uintptr_t a = (uintptr_t)p;
+    const uint64_t* q = (const uint64_t*)(a & ~(uintptr_t)7);
+    uint32_t sh = (uint32_t)(a & 7) * 8;
+    uint64_t lo = q[0], hi = q[1];
+    return sh ? (lo >> sh) | (hi << (64 - sh)) : lo;
+}
+
 // hash2 "last occurrence" (BinTree.java:183-193) without a sort: hash2 has only
 // 1024 values, so one wave sweeps its stream in position order with the heads in
 // LDS. Per round of 64 positions, one ballot per hash bit gives each lane the lanes
 // with its hash (wave-level multi-split); the nearest of them below the lane is its
 // predecessor, else the head, and the highest of them updates the head. Reads of
-// k2 and writes of prev2 are coalesced (position order).
+// k2 are coalesced (position order).
+// The same sweep emits the walk's inputs of every position, in position order (coalesced),
+// into the position's own match-list record (the walk reads it before it writes the record):
+// the first 16 bytes of the suffix, the hash2 and hash3 "last occurrence" (prev3 comes from
+// mf_prev_kernel, which runs first) and whether their first bytes equal the position's
+// (BinTree.java:184-207). A member then costs the walk one load of its record instead of
+// five scattered loads (prefix, two candidates, their bytes).
 __global__ void __launch_bounds__(64) mf_prev2_kernel(const uint64_t* __restrict__ offs, const uint32_t* __restrict__ k2,
-                                                      uint32_t* __restrict__ prev2) {
+                                                      const uint8_t* __restrict__ in, const uint32_t* __restrict__ prev3,
+                                                      v4u32* __restrict__ recs, uint32_t rec_vecs) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];   // dynamic LDS (the CPU emulation shares it)
-    uint32_t* head = (uint32_t*)smem;                                   // [1024]
+    uint32_t* head = (uint32_t*)smem;                                   // [1024] last position per hash2
+    uint8_t* hbyte = smem + 1024 * 4;                                   // [1024] its first byte
     const uint32_t lane = threadIdx.x;
-    for (uint32_t k = lane; k < 1024; k += 64) head[k] = kNoPos;
+    for (uint32_t k = lane; k < 1024; k += 64) { head[k] = kNoPos; hbyte[k] = 0; }
     __syncthreads();
     const uint32_t s = blockIdx.x;
     const uint64_t lo = offs[s], n = offs[s + 1] - lo;
-    uint32_t nkey = lane < n ? k2[lo + lane] : kSentinel32;   // the next round's key is loaded a round ahead
+    // Software pipeline: a round's prefix and hash3 byte are loaded during the round
+    // before it, its key and prev3 two rounds ahead (the byte load depends on them: prev3
+    // is defined where the key is live); the hash2 candidate's byte comes from the
+    // candidate's lane (same round) or from LDS (head).
+    auto key2 = [&](uint64_t i) { return i < n ? k2[lo + i] : kSentinel32; };
+    auto pos3 = [&](uint64_t i) { return i < n ? prev3[lo + i] : kNoPos; };
+    auto byte3 = [&](uint32_t k, uint32_t p) { return k != kSentinel32 && p != kNoPos ? (uint32_t)in[p] : 0u; };
+    uint32_t nkey = key2(lane), nnkey = key2(lane + 64);
+    uint64_t nc0 = load8(in + lo + lane), nc1 = load8(in + lo + lane + 8);   // the batch copy is padded
+    uint32_t np3 = pos3(lane), nnp3 = pos3(lane + 64);
+    uint32_t nb3 = byte3(nkey, np3);
     for (uint64_t r0 = 0; r0 < n; r0 += 64) {
         const uint64_t i = r0 + lane;
-        const uint32_t key = nkey;
-        nkey = i + 64 < n ? k2[lo + i + 64] : kSentinel32;
+        const uint32_t key = nkey, p3 = np3, b3 = nb3;
+        const uint64_t c0 = nc0, c1 = nc1;
+        if (r0 + 64 < n) {
+            nc0 = load8(in + lo + i + 64); nc1 = load8(in + lo + i + 72);
+            nb3 = byte3(nnkey, nnp3);
+            nkey = nnkey; np3 = nnp3;
+            nnkey = key2(i + 128); nnp3 = pos3(i + 128);
+        }
         const bool live = key != kSentinel32;   // sentinel: no insertion, no prev (as mf_prev_kernel)
         const uint32_t d = key & 1023u;
         uint64_t peers = __ballot(live);
@@ -126,11 +159,20 @@ __global__ void __launch_bounds__(64) mf_prev2_kernel(const uint64_t* __restrict
         }
         const uint64_t below = peers & ((1ull << lane) - 1);   // lane < 64
         const uint64_t above = lane == 63 ? 0ull : (peers & ~((2ull << lane) - 1));
+        const uint32_t cur0 = (uint32_t)(c0 & 0xFFu);
+        const uint32_t src = below ? 63u - (uint32_t)__builtin_clzll(below) : lane;
+        const uint32_t bsh = (uint32_t)__shfl((int)cur0, (int)src);   // every lane takes part
         const uint32_t hd = live ? head[d] : kNoPos;
+        const uint32_t hb = live ? (uint32_t)hbyte[d] : 0u;
         __builtin_amdgcn_wave_barrier();
         if (live) {
-            prev2[lo + i] = below ? (uint32_t)(lo + r0) + (63u - (uint32_t)__builtin_clzll(below)) : hd;
-            if (above == 0) head[d] = (uint32_t)(lo + i);
+            const uint32_t p2 = below ? (uint32_t)(lo + r0) + src : hd;
+            const uint32_t b2 = below ? bsh : hb;
+            if (above == 0) { head[d] = (uint32_t)(lo + i); hbyte[d] = (uint8_t)cur0; }
+            const uint32_t f2 = p2 != kNoPos && b2 == cur0, f3 = p3 != kNoPos && b3 == cur0;
+            v4u32* rp = recs + (lo + i) * rec_vecs;
+            rp[0] = v4u32{(uint32_t)c0, (uint32_t)(c0 >> 32), (uint32_t)c1, (uint32_t)(c1 >> 32)};
+            rp[1] = v4u32{p2, p3, f2 | (f3 << 1), 0u};
         }
         __builtin_amdgcn_wave_barrier();
     }
@@ -264,14 +306,6 @@ __global__ void __launch_bounds__(kChainThreads) mf_chain_scan_kernel(const uint
     if (tid == 0) chain_offs[nstreams] = run;
 }
 
-// Unaligned 8-byte little-endian load from a buffer padded by >= 16 bytes.
-__device__ inline uint64_t load8(const uint8_t* p) {
-    uintptr_t a = (uintptr_t)p;
-    const uint64_t* q = (const uint64_t*)(a & ~(uintptr_t)7);
-    uint32_t sh = (uint32_t)(a & 7) * 8;
-    uint64_t lo = q[0], hi = q[1];
-    return sh ? (lo >> sh) | (hi << (64 - sh)) : lo;
-}
 
 // First index r in [from, limit) with a[r] != b[r] (limit if none); when r < limit,
 // *a_less = a[r] < b[r]. 16 bytes per iteration: both sides' words are loaded in
@@ -429,34 +463,32 @@ __global__ void __launch_bounds__(64) LZG_WALK_ATTR mf_walk_kernel(const uint8_t
     // prefix, its hash2/hash3 candidates' first bytes) and the candidates of member
     // i + 2 are loaded at the start of member i, so they arrive while member i walks
     // the tree instead of in front of member i + 1's walk.
-    const uint32_t* __restrict__ prev2 = a.prev2;
-    const uint32_t* __restrict__ prev3 = a.prev3;
-    auto cand = [&](uint64_t gi, uint32_t& v2, uint32_t& v3) {
-        v2 = BT4 ? __builtin_nontemporal_load(prev2 + gi) : kNoPos;
-        v3 = BT4 ? __builtin_nontemporal_load(prev3 + gi) : kNoPos;
-    };
-    auto cand_bytes = [&](uint32_t v2, uint32_t v3, uint32_t& b2, uint32_t& b3) {
-        b2 = BT4 && v2 != kNoPos ? (uint32_t)in[v2] : 0u;   // first byte of the candidate (batch-global index)
-        b3 = BT4 && v3 != kNoPos ? (uint32_t)in[v3] : 0u;
+    // BT4: a member's inputs (prefix, hash2 / hash3 candidates and whether their first
+    // bytes match) are one 32-byte load of its record, written in position order by
+    // mf_prev2_kernel; BT2 has no candidates and loads its prefix from the stream
+    const uint32_t rv = a.rec_vecs;
+    auto member_in = [&](uint64_t gi, uint64_t& c0_, uint64_t& c1_, uint32_t& v2_, uint32_t& v3_, uint32_t& f_) {
+        if (BT4) {
+            const v4u32* rp = recs + gi * rv;
+            const v4u32 x0 = __builtin_nontemporal_load(rp), x1 = __builtin_nontemporal_load(rp + 1);
+            c0_ = (uint64_t)x0[0] | ((uint64_t)x0[1] << 32); c1_ = (uint64_t)x0[2] | ((uint64_t)x0[3] << 32);
+            v2_ = x1[0]; v3_ = x1[1]; f_ = x1[2];
+        } else {
+            c0_ = load8(sb + (gi - base)); c1_ = load8(sb + (gi - base) + 8);
+            v2_ = v3_ = kNoPos; f_ = 0;
+        }
     };
     uint64_t g = vals4[start];
     uint64_t g1 = start + 1 < end ? vals4[start + 1] : 0, g2 = start + 2 < end ? vals4[start + 2] : 0;
-    uint32_t pv2, pv3, pv2n = kNoPos, pv3n = kNoPos, b2, b3;
-    cand(g, pv2, pv3);
-    if (start + 1 < end) cand(g1, pv2n, pv3n);
-    uint64_t c0 = load8(sb + (g - base)), c1 = load8(sb + (g - base) + 8);   // this member's prefix
-    cand_bytes(pv2, pv3, b2, b3);
+    uint64_t c0, c1;
+    uint32_t pv2, pv3, fl;
+    member_in(g, c0, c1, pv2, pv3, fl);
     for (uint64_t i = start; i < end; i++) {
         if (g - base >= n) { *err = 4; return; }   // a member outside its chain's stream
         const uint64_t g3 = i + 3 < end ? vals4[i + 3] : 0;
-        uint32_t pv2nn = kNoPos, pv3nn = kNoPos, b2n = 0, b3n = 0;
         uint64_t c0n = 0, c1n = 0;
-        if (i + 2 < end) cand(g2, pv2nn, pv3nn);
-        if (i + 1 < end) {
-            c0n = load8(sb + (g1 - base));
-            c1n = load8(sb + (g1 - base) + 8);
-            cand_bytes(pv2n, pv3n, b2n, b3n);
-        }
+        uint32_t pv2n = kNoPos, pv3n = kNoPos, fln = 0;
+        if (i + 1 < end) member_in(g1, c0n, c1n, pv2n, pv3n, fln);   // arrives while member i walks
         uint32_t p = (uint32_t)(g - base);
         uint32_t pos = p + 1;               // BinTree 1-based position
         uint64_t rem = n - p;
@@ -491,13 +523,12 @@ __global__ void __launch_bounds__(64) LZG_WALK_ATTR mf_walk_kernel(const uint8_t
             last_d = d;
             cnt++;
         };
-        const uint32_t cur0 = (uint32_t)(c0 & 0xFFu);
-        if (BT4) {   // hash2 / hash3 candidates, BinTree.java:183-207
+        if (BT4) {   // hash2 / hash3 candidates, BinTree.java:183-207 (the byte checks: mf_prev2_kernel)
             uint32_t cm2 = pv2 == kNoPos ? 0 : (uint32_t)(pv2 - base) + 1;
             uint32_t cm3 = pv3 == kNoPos ? 0 : (uint32_t)(pv3 - base) + 1;
-            if (cm2 > match_min && b2 == cur0) { max_len = 2; emit(2, pos - cm2 - 1); }
+            if (cm2 > match_min && (fl & 1u)) { max_len = 2; emit(2, pos - cm2 - 1); }
             const uint32_t d2 = pos - cm2 - 1;   // the len-2 pair's distance, if it was emitted
-            if (cm3 > match_min && b3 == cur0) {
+            if (cm3 > match_min && (fl & 2u)) {
                 if (cm3 == cm2) cnt--;
                 max_len = 3;
                 emit(3, pos - cm3 - 1);
@@ -583,8 +614,7 @@ __global__ void __launch_bounds__(64) LZG_WALK_ATTR mf_walk_kernel(const uint8_t
         prev_local = pos;
         g = g1; g1 = g2; g2 = g3;
         c0 = c0n; c1 = c1n;
-        pv2 = pv2n; pv3 = pv3n; pv2n = pv2nn; pv3n = pv3nn;
-        b2 = b2n; b3 = b3n;
+        pv2 = pv2n; pv3 = pv3n; fl = fln;
     }
 }
 
@@ -608,7 +638,7 @@ static MfArgs mf_args(const Derived& d, const MfBuffers& w, uint64_t total, int 
         unsigned lo = 0, hi = 0xFFFFFFFFu;
         if (sscanf(e, "%u,%u", &lo, &hi) >= 1) { a.walk_lo = lo; a.walk_hi = hi; }
     }
-    a.k4 = w.k4; a.k3 = (uint32_t*)w.k3; a.k2 = (uint32_t*)w.k2; a.vals = w.vals; a.mrec = w.pairs; a.rec_vecs = wide_pairs ? rec_vecs<uint64_t>() : rec_vecs<uint32_t>(); a.prev2 = w.prev2; a.prev3 = w.prev3;
+    a.k4 = w.k4; a.k3 = (uint32_t*)w.k3; a.k2 = (uint32_t*)w.k2; a.vals = w.vals; a.mrec = w.pairs; a.rec_vecs = wide_pairs ? rec_vecs<uint64_t>() : rec_vecs<uint32_t>(); a.prev3 = w.prev3;
     return a;
 }
 
@@ -641,14 +671,15 @@ int mf_front(Ctx* ctx, const Derived& d, const uint8_t* in, const uint64_t* d_of
     if (bt4) {
         const unsigned prev_grid = (unsigned)(((total + B - 1) / B + 7) & ~7ull);   // total < 2^32: fits
         {
-            TimedLaunch tl(ctx, "mf_prev2", st);
-            hipLaunchKernelGGL(mf_prev2_kernel, dim3(nstreams), dim3(64), 1024 * 4, st, d_offs, (const uint32_t*)w.k2, w.prev2);
-        }
-        {
             TimedLaunch tl(ctx, "mf_sort", st);
             if ((rc = seg_radix_sort(ctx, false, w.k3, w.vals, w.ks, w.vs, w.son, w.son + total, w.hist, total, d_offs, nstreams, 16, st))) return rc;
         }
         hipLaunchKernelGGL(mf_prev_kernel, dim3(prev_grid), dim3(B), 0, st, (const uint32_t*)w.ks, w.vs, total, w.prev3);
+        {   // after mf_prev: the walk-input records carry both candidates
+            TimedLaunch tl(ctx, "mf_prev2", st);
+            hipLaunchKernelGGL(mf_prev2_kernel, dim3(nstreams), dim3(64), 1024 * 5, st, d_offs, (const uint32_t*)w.k2, in,
+                               (const uint32_t*)w.prev3, w.pairs, a.rec_vecs);
+        }
     }
     {
         TimedLaunch tl(ctx, "mf_sort", st);

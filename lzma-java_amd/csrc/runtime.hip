@@ -185,7 +185,7 @@ static int pass_carve(Ctx* ctx, EncPass& P) {
     auto phase1 = [&](Carver& c, MfBuffers& w) {   // buffers only the match finder uses
         w.k4 = c.take<uint64_t>(T); w.k3 = c.take<uint64_t>(T); w.k2 = c.take<uint64_t>(T); w.ks = c.take<uint64_t>(T);
         w.vals = c.take<uint32_t>(T); w.vs = c.take<uint32_t>(T);
-        w.prev2 = c.take<uint32_t>(T); w.prev3 = c.take<uint32_t>(T);
+        w.prev3 = c.take<uint32_t>(T);
         w.flag = c.take<uint8_t>(T);
         w.chain_start = c.take<uint32_t>(T); w.chain_len = c.take<uint32_t>(T); w.long_list = c.take<uint32_t>(T);
         w.chain_idx = c.take<uint32_t>(T); w.chain_order = c.take<uint32_t>(T);

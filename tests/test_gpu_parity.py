@@ -577,7 +577,7 @@ def test_gpu_single_stream_c_abi(ctx):
     assert rc == lzma_amd.LZMA_E_OVERFLOW
 
 
-@pytest.mark.timeout(600)
+@pytest.mark.timeout(int(os.environ.get("LZMA_CONFIG4_TIMEOUT", "600")))
 def test_gpu_config4_shape_one_stream_longer_than_dict(ctx, heartbeat):
     """Config 4's regime: ONE BENCH stream far longer than a chunk and longer than its
     dictionary (72 MiB at dict 2^26, L5), so the window expires for the last 8 MiB
