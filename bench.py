@@ -87,10 +87,12 @@ def parse():
                     help="run each step's encode and decode back to back (default: pipelined, step k's decode on "
                          "its own HIP stream and context beside step k+1's match finder; step k+1's parser starts "
                          "when that decode is done, lzma_ctx_set_parse_fence; see --pipeline)")
-    ap.add_argument("--pipeline", choices=["split", "decode"], default="decode",
-                    help="pipelined schedule: decode (default) = step k's pack + decode beside step k+1's match "
-                         "finder, with the synchronous encode; split = the split encode, step k's range coder "
-                         "beside them too (measured the same: profiles/r04/ab_bench_split_encode_vs_decode_overlap.jsonl)")
+    ap.add_argument("--pipeline", choices=["split", "decode"], default="split",
+                    help="pipelined schedule: split (default) = the split encode: step k's range coder, pack and "
+                         "decode beside step k+1's match finder (without a parse fence, its walk enqueued as soon "
+                         "as its sorts are done); decode = the synchronous encode, step k's pack + decode beside "
+                         "step k+1's match finder. Measured equal at 4096 streams, split 525 -> 513 ms per step "
+                         "at the 8-way share (profiles/r05/strong_share*.jsonl, pipe_ab.jsonl)")
     ap.add_argument("--emulate", action="store_true",
                     help="CPU tests only: CPU tensors, gloo and the SIMT-emulated product kernels (measures nothing)")
     ap.add_argument("--project-share", type=int, default=1,

@@ -94,11 +94,14 @@ int lzma_pack_dev(lzma_ctx *ctx, const uint8_t *d_src, const uint64_t *h_src_off
  * match finder runs on the caller's stream.
  *   lzma_enc_stage_dev: stages the batch (arguments as lzma_enc_batch_dev; d_in and
  *     d_out must stay valid until _wait) and enqueues its match finder's keys, sorts
- *     and chain lists on hip_stream; returns without waiting.
- *   lzma_enc_parse_dev_async: the walk (it reads the chain count and the walk's
- *     verdict back: waits for the match finder), then the parser on hip_stream (after
- *     the parse fence's decode, if any), then the range coder on the coder stream;
- *     returns without waiting for the parser or the coder.
+ *     and chain lists on hip_stream. Without a parse fence it also enqueues the walk,
+ *     whose grid is sized by a host read of the chain count: it then waits for the work
+ *     ahead on hip_stream and the sorts (not for the walk). With a fence it returns
+ *     without waiting.
+ *   lzma_enc_parse_dev_async: the walk if the staging did not enqueue it (it reads the
+ *     chain count back), waits for the walk's verdict, then enqueues the parser on
+ *     hip_stream (after the parse fence's decode, if any) and the range coder on the
+ *     coder stream; returns without waiting for the parser or the coder.
  *   lzma_enc_parse_dev_wait: waits for the coder; h_out_lens as lzma_enc_batch_dev.
  * One pass only: at most 16384 streams and lzma_ctx_set_batch_bytes of input
  * (LZMA_E_PARAM otherwise). Order: stage, parse_async, then either wait or the next

@@ -706,8 +706,10 @@ int mf_front(Ctx* ctx, const Derived& d, const uint8_t* in, const uint64_t* d_of
     return LZMA_OK;
 }
 
-int mf_back(Ctx* ctx, const Derived& d, const uint8_t* in, const uint64_t* d_offs, int nstreams, uint64_t total,
-            bool wide_pairs, MfBuffers& w, hipStream_t st) {
+int mf_walk_launch(Ctx* ctx, const Derived& d, const uint8_t* in, const uint64_t* d_offs, int nstreams, uint64_t total,
+                   bool wide_pairs, MfBuffers& w, hipStream_t st) {
+    if (!ctx->pin_mf.ensure(16)) return ctx->fail(LZMA_E_NOMEM, "pinned staging");
+    *(int32_t*)(ctx->pin_mf.as<uint64_t>() + 1) = 0;   // the walk's verdict (no walk: none)
     if (total == 0) return LZMA_OK;
     MfArgs a = mf_args(d, w, total, nstreams, wide_pairs);
     const bool bt4 = d.hash_array != 0;
@@ -715,7 +717,6 @@ int mf_back(Ctx* ctx, const Derived& d, const uint8_t* in, const uint64_t* d_off
     uint32_t* long_raw = (uint32_t*)w.k4;
     const uint32_t long_min = mf_long_min();
     // sizes the walk grid: one host round trip per pass (pinned: see HostBuf)
-    if (!ctx->pin_mf.ensure(16)) return ctx->fail(LZMA_E_NOMEM, "pinned staging");
     uint64_t* p_cnt = ctx->pin_mf.as<uint64_t>();
     if (hipMemcpyAsync(p_cnt, w.chain_offs + nstreams, 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
         hipMemcpyAsync(p_cnt + 1, w.cls + 64, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
@@ -753,12 +754,26 @@ int mf_back(Ctx* ctx, const Derived& d, const uint8_t* in, const uint64_t* d_off
     }
     LZG_TRACE(ctx, st, "mf_walk done (%llu chains)", (unsigned long long)nchains);
     int32_t* p_err = (int32_t*)(p_cnt + 1);
-    hipMemcpyAsync(p_err, w.err, sizeof(int), hipMemcpyDeviceToHost, st);
-    if (hipStreamSynchronize(st) != hipSuccess) return ctx->fail(LZMA_E_DEVICE, "mf_walk: %s", hipGetErrorString(hipGetLastError()));
-    if (*p_err == 3) return ctx->fail(LZMA_E_INTERNAL, "mf_walk: a tree link outside its bucket");
-    if (*p_err == 4) return ctx->fail(LZMA_E_INTERNAL, "mf_walk: a chain list entry out of range (index, extent, stream or member)");
-    if (*p_err) return LZMA_E_OVERFLOW;   // caller grows the overflow pool and retries
+    if (hipMemcpyAsync(p_err, w.err, sizeof(int), hipMemcpyDeviceToHost, st) != hipSuccess)
+        return ctx->fail(LZMA_E_DEVICE, "mf_walk: %s", hipGetErrorString(hipGetLastError()));
     return LZMA_OK;
+}
+
+// the walk's verdict, once the stream that launched it has passed its verdict copy
+int mf_walk_result(Ctx* ctx) {
+    const int32_t e = *(const int32_t*)(ctx->pin_mf.as<uint64_t>() + 1);
+    if (e == 3) return ctx->fail(LZMA_E_INTERNAL, "mf_walk: a tree link outside its bucket");
+    if (e == 4) return ctx->fail(LZMA_E_INTERNAL, "mf_walk: a chain list entry out of range (index, extent, stream or member)");
+    if (e) return LZMA_E_OVERFLOW;   // caller grows the overflow pool and retries
+    return LZMA_OK;
+}
+
+int mf_back(Ctx* ctx, const Derived& d, const uint8_t* in, const uint64_t* d_offs, int nstreams, uint64_t total,
+            bool wide_pairs, MfBuffers& w, hipStream_t st) {
+    int rc = mf_walk_launch(ctx, d, in, d_offs, nstreams, total, wide_pairs, w, st);
+    if (rc) return rc;
+    if (hipStreamSynchronize(st) != hipSuccess) return ctx->fail(LZMA_E_DEVICE, "mf_walk: %s", hipGetErrorString(hipGetLastError()));
+    return mf_walk_result(ctx);
 }
 
 }  // namespace lzg

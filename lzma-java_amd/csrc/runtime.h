@@ -162,6 +162,7 @@ struct Ctx {
     int split_state = 0;                   // 0 idle, 1 staged, 2 parsed (coder in flight)
     int rc_pending = 0;                    // streams of the coder in flight
     hipEvent_t rc_done = nullptr, parse_done = nullptr;
+    hipEvent_t walk_done = nullptr;        // the split form: the staged walk's verdict copied to the host
     hipStream_t rc_stream = nullptr;       // created on first use
     DevBuf split_recs, split_coder;        // the coder's records and per-stream arrays (apart from the arena)
     HostBuf pin_rc;                        // the coder's lengths and verdicts
@@ -314,6 +315,12 @@ int mf_front(Ctx* ctx, const Derived& d, const uint8_t* in, const uint64_t* d_of
              bool wide_pairs, MfBuffers& w, hipStream_t st);
 int mf_back(Ctx* ctx, const Derived& d, const uint8_t* in, const uint64_t* d_offs, int nstreams, uint64_t total,
             bool wide_pairs, MfBuffers& w, hipStream_t st);
+// mf_back in two halves: the walk and its verdict's copy enqueued on st (one host round
+// trip sizes the grid), then the verdict once st has passed that copy (the split encode
+// checks it when the parse is enqueued, so the walk runs while the host does other work)
+int mf_walk_launch(Ctx* ctx, const Derived& d, const uint8_t* in, const uint64_t* d_offs, int nstreams, uint64_t total,
+                   bool wide_pairs, MfBuffers& w, hipStream_t st);
+int mf_walk_result(Ctx* ctx);
 // sort.hip: stable per-stream radix sort by the low end_bit key bits
 int seg_radix_sort(Ctx* ctx, bool key64, const void* kin, const uint32_t* vin, void* kout, uint32_t* vout,
                    uint64_t* tmp_a, uint64_t* tmp_b, uint32_t* hist, uint64_t n, const uint64_t* d_offs, int nstreams,

@@ -120,6 +120,7 @@ struct EncPass {
     int ns = 0;
     uint64_t in0 = 0, total = 0;
     bool wide = false, split = false;
+    bool walk_launched = false;   // the split form: the walk was enqueued by the staging
     size_t psz = 4;
     std::vector<uint64_t> offs, oofs, rofs;
     std::vector<uint32_t> order;
@@ -279,9 +280,16 @@ static int pass_stage(Ctx* ctx, EncPass& P, hipStream_t st) {
 
 // the walk; on a full overflow pool, grow it (4x, remembered by the context) and run the
 // pass's match finder again from the staging. Returns LZMA_OK or an error.
-static int pass_mf_back(Ctx* ctx, EncPass& P, hipStream_t st) {
+// launched: the walk was already enqueued (the split form's staging), with walk_done
+// recorded behind its verdict copy.
+static int pass_mf_back(Ctx* ctx, EncPass& P, hipStream_t st, bool launched = false) {
     for (int attempt = 0; attempt < 6; attempt++) {
-        int rc = mf_back(ctx, P.d, P.inpad, P.d_offs, P.ns, P.total, P.wide, P.w, st);
+        int rc;
+        if (launched) {
+            launched = false;
+            HIPCHK(hipEventSynchronize(ctx->walk_done));
+            rc = mf_walk_result(ctx);
+        } else rc = mf_back(ctx, P.d, P.inpad, P.d_offs, P.ns, P.total, P.wide, P.w, st);
         if (rc != LZMA_E_OVERFLOW) return rc;
         if (P.slots_per_k >= 1024) return ctx->fail(LZMA_E_INTERNAL, "overflow pool full at one slot per position");
         P.slots_per_k = std::min<uint64_t>(1024, P.slots_per_k * 4);
@@ -477,9 +485,27 @@ static int enc_stage_dev(Ctx* ctx, const lzma_params* p, const uint8_t* d_in, co
     EncPass& P = *ctx->split_pass;
     P = EncPass();
     pass_plan(ctx, P, d, d_in, h_offs, 0, nstreams, d_out, h_out_offs, true);
+    if (!ctx->walk_done && hipEventCreateWithFlags(&ctx->walk_done, hipEventDisableTiming) != hipSuccess)
+        return ctx->fail(LZMA_E_DEVICE, "walk event");
     if ((rc = pass_carve(ctx, P)) || (rc = pass_stage(ctx, P, st)) ||
         (rc = mf_front(ctx, P.d, P.inpad, P.d_offs, P.ns, P.total, P.wide, P.w, st)))
         return rc;
+    // Without a parse fence, the walk too: it then runs as soon as the sorts are done
+    // (behind the previous batch's parser on st) instead of when the caller next enqueues a
+    // parse, after collecting the previous batch's coder. Its grid is sized by a host read
+    // of the chain count, so this call then waits for the work ahead of it on st. With a
+    // fence, the caller's decode is on the critical path and must not wait behind that: the
+    // walk stays in lzma_enc_parse_dev_async.
+    bool fenced;
+    {
+        std::lock_guard<std::mutex> g(g_ctx_lock);
+        fenced = ctx->fence != nullptr;
+    }
+    if (!fenced) {
+        if ((rc = mf_walk_launch(ctx, P.d, P.inpad, P.d_offs, P.ns, P.total, P.wide, P.w, st))) return rc;
+        HIPCHK(hipEventRecord(ctx->walk_done, st));
+        P.walk_launched = true;
+    }
     ctx->split_state = 1;
     return LZMA_OK;
 }
@@ -490,7 +516,7 @@ static int enc_parse_dev_async(Ctx* ctx, hipStream_t st) {
     EncPass& P = *ctx->split_pass;
     ctx->split_state = 0;   // from here on the staged pass is consumed (or failed)
     int rc;
-    if ((rc = pass_mf_back(ctx, P, st)) || (rc = pass_parse(ctx, P, st))) return rc;
+    if ((rc = pass_mf_back(ctx, P, st, P.walk_launched)) || (rc = pass_parse(ctx, P, st))) return rc;
     if (!ctx->rc_stream && hipStreamCreateWithFlags(&ctx->rc_stream, hipStreamNonBlocking) != hipSuccess)
         return ctx->fail(LZMA_E_DEVICE, "coder stream");
     if (!ctx->parse_done && hipEventCreateWithFlags(&ctx->parse_done, hipEventDisableTiming) != hipSuccess)
@@ -755,6 +781,7 @@ void lzma_ctx_destroy(lzma_ctx* ctx) {
     if (ctx->split_state) hipDeviceSynchronize();   // a staged pass's match finder may still run
     if (ctx->rc_done) hipEventDestroy(ctx->rc_done);
     if (ctx->parse_done) hipEventDestroy(ctx->parse_done);
+    if (ctx->walk_done) hipEventDestroy(ctx->walk_done);
     if (ctx->rc_stream) hipStreamDestroy(ctx->rc_stream);
     delete ctx->split_pass;
     ctx->split_recs.release();

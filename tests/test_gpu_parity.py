@@ -269,15 +269,21 @@ def test_gpu_split_encode_pipelined_order():
         c.close()
 
 
-def test_gpu_split_encode_heterogeneous_batches():
+@pytest.mark.parametrize("fenced", [False, True])
+def test_gpu_split_encode_heterogeneous_batches(fenced):
     """The split encode with batches of DIFFERENT layouts: batch B has more
     streams, ragged sizes and a larger total than batch A, and is staged -- its offsets,
     order and status rewritten into the pass arrays, its match finder enqueued -- while
     batch A's range coder may still run on the coder stream. Both batches byte-equal to the
     oracle's Encoder.Code. Guards the copy of the coder's per-stream arrays, which must be
-    ordered before the next stage's rewrites (runtime.hip enc_parse_dev_async)."""
+    ordered before the next stage's rewrites (runtime.hip enc_parse_dev_async). Unfenced,
+    the staging also enqueues the walk (behind batch A's parser); fenced (a decoder
+    context as the parse fence), the walk waits for lzma_enc_parse_dev_async."""
     torch = pytest.importorskip("torch")
     c = lzma_amd.Context(0)
+    dec = lzma_amd.Context(0) if fenced else None
+    if fenced:
+        c.set_parse_fence(dec)
     try:
         p = lzma_amd.make_params(dict_size=1 << 26, fb=32)
         st = torch.cuda.current_stream().cuda_stream
@@ -307,6 +313,9 @@ def test_gpu_split_encode_heterogeneous_batches():
             for i in range(n):
                 assert h[int(oo[i]):int(oo[i] + lens[i])].tobytes() == refs[i], (n, i)
     finally:
+        if fenced:
+            c.set_parse_fence(None)
+            dec.close()
         c.close()
 
 
