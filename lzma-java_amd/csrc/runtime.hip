@@ -516,7 +516,9 @@ static int enc_parse_dev_async(Ctx* ctx, hipStream_t st) {
     EncPass& P = *ctx->split_pass;
     ctx->split_state = 0;   // from here on the staged pass is consumed (or failed)
     int rc;
-    if ((rc = pass_mf_back(ctx, P, st, P.walk_launched)) || (rc = pass_parse(ctx, P, st))) return rc;
+    if ((rc = pass_mf_back(ctx, P, st, P.walk_launched))) return rc;
+    if (exp_env("LZG_PROBE_WALK_ONLY")) return LZMA_OK;   // experiment build: concurrency probe (tools/overlap_probe.py)
+    if ((rc = pass_parse(ctx, P, st))) return rc;
     if (!ctx->rc_stream && hipStreamCreateWithFlags(&ctx->rc_stream, hipStreamNonBlocking) != hipSuccess)
         return ctx->fail(LZMA_E_DEVICE, "coder stream");
     if (!ctx->parse_done && hipEventCreateWithFlags(&ctx->parse_done, hipEventDisableTiming) != hipSuccess)
