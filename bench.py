@@ -89,10 +89,11 @@ def parse():
                          "when that decode is done, lzma_ctx_set_parse_fence; see --pipeline)")
     ap.add_argument("--pipeline", choices=["split", "decode"], default="split",
                     help="pipelined schedule: split (default) = the split encode: step k's range coder, pack and "
-                         "decode beside step k+1's match finder (without a parse fence, its walk enqueued as soon "
-                         "as its sorts are done); decode = the synchronous encode, step k's pack + decode beside "
-                         "step k+1's match finder. Measured equal at 4096 streams, split 525 -> 513 ms per step "
-                         "at the 8-way share (profiles/r05/strong_share*.jsonl, pipe_ab.jsonl)")
+                         "decode beside step k+1's match finder; at <= 8 streams per CU (no parse fence) two "
+                         "batches are staged and step k+1's walk runs beside step k's parser; decode = the "
+                         "synchronous encode, step k's pack + decode beside step k+1's match finder. Measured: "
+                         "4096 streams 871 vs 884 ms per step, the 8-way share 508 vs 537 ms "
+                         "(profiles/r05/pipe_ab.jsonl, strong_share*.jsonl)")
     ap.add_argument("--emulate", action="store_true",
                     help="CPU tests only: CPU tensors, gloo and the SIMT-emulated product kernels (measures nothing)")
     ap.add_argument("--project-share", type=int, default=1,
@@ -238,22 +239,39 @@ def run_pass(args, D, p, ctxs, strong, rank, world, dist):
         if state.pop("dec_inflight", False):
             check_dec(*ctx_dec.decode_batch_dev_wait())
 
-    def step(k, nxt):
+    def stage():
+        ctx.encode_stage_dev(d_in, offs, p, d_comp, cap_offs, st)
+        state["staged"] = state.get("staged", 0) + 1
+
+    def step(k, ahead):   # ahead: the steps after this one in the same loop
         t0 = time.perf_counter()
         buf = d_packs[k % 2]
-        if overlap and args.pipeline == "split":
-            # the split encode: step k's walk and parser on st (the parser after step k-1's
-            # decode), its range coder on the encoder context's coder stream; step k+1's
-            # match finder is staged behind the parser and runs beside that coder and
-            # beside step k's pack + decode (decoder context, st_dec)
+        if overlap and args.pipeline == "split" and fence:
+            # 16 streams per CU: the parser fills the CUs and waits for step k-1's decode.
+            # Step k's walk and parser on st, its range coder on the encoder context's coder
+            # stream; step k+1's keys and sorts are staged behind the parser and run beside
+            # that coder and step k's pack + decode (decoder context, st_dec)
             if not state.get("staged"):
-                ctx.encode_stage_dev(d_in, offs, p, d_comp, cap_offs, st)
+                stage()
             ctx.encode_parse_dev_async(st)
-            state["staged"] = nxt
-            if nxt:
-                ctx.encode_stage_dev(d_in, offs, p, d_comp, cap_offs, st)
+            state["staged"] -= 1
+            if ahead:
+                stage()
             lens = ctx.encode_parse_dev_wait()
-            join()   # step k-1's decode: done (step k's parser waited for it)
+        elif overlap and args.pipeline == "split":
+            # <= 8 streams per CU: two batches staged. Step k+1's keys and sorts ran on st
+            # ahead of step k's parser, its walk runs on the encoder context's walk stream
+            # beside that parser (the walk needs no LDS); step k+2's keys and sorts follow the
+            # parser on st at once (not after the host has collected step k's coder)
+            while state.get("staged", 0) < 1 + min(ahead, 1):
+                stage()
+            ctx.encode_parse_dev_async(st)
+            state["staged"] -= 1
+            if ahead >= 2:
+                stage()
+            lens = ctx.encode_parse_dev_wait()
+        if overlap and args.pipeline == "split":
+            join()   # step k-1's decode (fenced: done, step k's parser waited for it)
             pk = ctx_dec.pack_dev(d_comp, cap_offs, lens, buf, st_dec)   # synchronous: buf is complete
         else:
             lens = ctx.encode_batch_dev(d_in, offs, p, d_comp, cap_offs, st)
@@ -275,7 +293,7 @@ def run_pass(args, D, p, ctxs, strong, rank, world, dist):
     # every step stages the next one inside its own time; the last step of each loop
     # stages nothing, so the timed loop holds exactly its own steps' work
     for k in range(args.warmup):
-        step(k, k + 1 < args.warmup)
+        step(k, args.warmup - 1 - k)
     join()
     for c in (ctx, ctx_dec):
         c.set_timing(True)
@@ -284,7 +302,7 @@ def run_pass(args, D, p, ctxs, strong, rank, world, dist):
     barrier()
     t0 = time.perf_counter()
     for k in range(args.steps):
-        step(k, k + 1 < args.steps)
+        step(k, args.steps - 1 - k)
     join()
     barrier()
     elapsed = time.perf_counter() - t0

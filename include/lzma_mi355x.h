@@ -91,25 +91,30 @@ int lzma_pack_dev(lzma_ctx *ctx, const uint8_t *d_src, const uint64_t *h_src_off
                   int nstreams, uint8_t *d_dst, const uint64_t *h_dst_offs, void *hip_stream);
 /* The same encode in three calls, for a caller that pipelines batches: the range
  * coder of one batch runs on the context's own coder stream while the next batch's
- * match finder runs on the caller's stream.
+ * match finder runs on the caller's stream, and the next batch's walk on the
+ * context's walk stream beside this batch's parser.
  *   lzma_enc_stage_dev: stages the batch (arguments as lzma_enc_batch_dev; d_in and
  *     d_out must stay valid until _wait) and enqueues its match finder's keys, sorts
- *     and chain lists on hip_stream. Without a parse fence it also enqueues the walk,
- *     whose grid is sized by a host read of the chain count: it then waits for the work
- *     ahead on hip_stream and the sorts (not for the walk). With a fence it returns
- *     without waiting.
- *   lzma_enc_parse_dev_async: the walk if the staging did not enqueue it (it reads the
- *     chain count back), waits for the walk's verdict, then enqueues the parser on
- *     hip_stream (after the parse fence's decode, if any) and the range coder on the
- *     coder stream; returns without waiting for the parser or the coder.
+ *     and chain lists on hip_stream. At most two batches are staged at once; a second
+ *     one's match finder runs after the first one's walk. A batch staged alone on a
+ *     context without a parse fence also gets its walk enqueued, whose grid is sized by
+ *     a host read of the chain count: the call then waits for the work ahead on
+ *     hip_stream and the sorts (not for the walk). Otherwise it returns without waiting.
+ *   lzma_enc_parse_dev_async: for the oldest staged batch: the walk if not enqueued yet
+ *     (it reads the chain count back), waits for the walk's verdict, then enqueues the
+ *     parser on hip_stream (after the parse fence's decode, if any) and the range coder
+ *     on the coder stream; then, if a second batch is staged, waits for its chain count
+ *     and enqueues its walk on the walk stream (beside this parser); returns without
+ *     waiting for the parser, the coder or that walk.
  *   lzma_enc_parse_dev_wait: waits for the coder; h_out_lens as lzma_enc_batch_dev.
- * One pass only: at most 16384 streams and lzma_ctx_set_batch_bytes of input
- * (LZMA_E_PARAM otherwise). Order: stage, parse_async, then either wait or the next
- * batch's stage (it may run while the coder is in flight) followed by wait; a second
- * parse_async before wait returns LZMA_E_PARAM. While a batch is staged or its coder
- * is in flight, the context's other encode, decode and pack entry points return
- * LZMA_E_PARAM. Reference: Encoder.Code (Encoder.java:1064-1077), as for
- * lzma_enc_batch_dev; the bytes are the same. */
+ * One pass per batch: at most 16384 streams and lzma_ctx_set_batch_bytes of input
+ * (LZMA_E_PARAM otherwise). Order: stage (once or twice), parse_async, wait, and so on,
+ * a stage of the next batch allowed anywhere while at most one other batch is staged
+ * (pipelined: stage k + 1, parse_async k, wait k); a second parse_async before wait, or
+ * a third staged batch, returns LZMA_E_PARAM, and a failed parse_async drops every
+ * staged batch. While a batch is staged or its coder is in flight, the context's other
+ * encode, decode and pack entry points return LZMA_E_PARAM. Reference: Encoder.Code
+ * (Encoder.java:1064-1077), as for lzma_enc_batch_dev; the bytes are the same. */
 int lzma_enc_stage_dev(lzma_ctx *ctx, const lzma_params *p,
                        const uint8_t *d_in, const uint64_t *h_offs, int nstreams,
                        uint8_t *d_out, const uint64_t *h_out_offs, void *hip_stream);

@@ -706,22 +706,37 @@ int mf_front(Ctx* ctx, const Derived& d, const uint8_t* in, const uint64_t* d_of
     return LZMA_OK;
 }
 
+// pinned words of a slot: [0] chain count, [1] long-chain count, [2] the walk's verdict
+static uint64_t* pin_slot(Ctx* ctx, int slot) { return ctx->pin_mf.as<uint64_t>() + 4 * slot; }
+
+int mf_count_enqueue(Ctx* ctx, const MfBuffers& w, int nstreams, hipStream_t st, int slot) {
+    if (!ctx->pin_mf.ensure(64)) return ctx->fail(LZMA_E_NOMEM, "pinned staging");
+    if (!ctx->cnt_done[slot] && hipEventCreateWithFlags(&ctx->cnt_done[slot], hipEventDisableTiming) != hipSuccess)
+        return ctx->fail(LZMA_E_DEVICE, "chain-count event");
+    uint64_t* p_cnt = pin_slot(ctx, slot);
+    p_cnt[0] = p_cnt[1] = 0;
+    p_cnt[2] = 0;   // the walk's verdict (no walk: none)
+    // sizes the walk grid: one host round trip per pass (pinned: see HostBuf)
+    if (w.chain_offs &&
+        (hipMemcpyAsync(p_cnt, w.chain_offs + nstreams, 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
+         hipMemcpyAsync(p_cnt + 1, w.cls + 64, 4, hipMemcpyDeviceToHost, st) != hipSuccess))
+        return ctx->fail(LZMA_E_DEVICE, "mf: chain count: %s", hipGetErrorString(hipGetLastError()));
+    if (hipEventRecord(ctx->cnt_done[slot], st) != hipSuccess)
+        return ctx->fail(LZMA_E_DEVICE, "mf: chain count: %s", hipGetErrorString(hipGetLastError()));
+    return LZMA_OK;
+}
+
 int mf_walk_launch(Ctx* ctx, const Derived& d, const uint8_t* in, const uint64_t* d_offs, int nstreams, uint64_t total,
-                   bool wide_pairs, MfBuffers& w, hipStream_t st) {
-    if (!ctx->pin_mf.ensure(16)) return ctx->fail(LZMA_E_NOMEM, "pinned staging");
-    *(int32_t*)(ctx->pin_mf.as<uint64_t>() + 1) = 0;   // the walk's verdict (no walk: none)
+                   bool wide_pairs, MfBuffers& w, hipStream_t st, int slot) {
+    if (hipEventSynchronize(ctx->cnt_done[slot]) != hipSuccess)
+        return ctx->fail(LZMA_E_DEVICE, "mf: chain count: %s", hipGetErrorString(hipGetLastError()));
     if (total == 0) return LZMA_OK;
     MfArgs a = mf_args(d, w, total, nstreams, wide_pairs);
     const bool bt4 = d.hash_array != 0;
     const unsigned B = 256;
     uint32_t* long_raw = (uint32_t*)w.k4;
     const uint32_t long_min = mf_long_min();
-    // sizes the walk grid: one host round trip per pass (pinned: see HostBuf)
-    uint64_t* p_cnt = ctx->pin_mf.as<uint64_t>();
-    if (hipMemcpyAsync(p_cnt, w.chain_offs + nstreams, 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
-        hipMemcpyAsync(p_cnt + 1, w.cls + 64, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
-        hipStreamSynchronize(st) != hipSuccess)
-        return ctx->fail(LZMA_E_DEVICE, "mf: chain count: %s", hipGetErrorString(hipGetLastError()));
+    uint64_t* p_cnt = pin_slot(ctx, slot);
     const uint64_t nchains = p_cnt[0];
     const uint32_t n_long = (uint32_t)p_cnt[1];   // the long chains (walked first)
     LZG_TRACE(ctx, st, "mf sorts + chain lists done");
@@ -753,15 +768,14 @@ int mf_walk_launch(Ctx* ctx, const Derived& d, const uint8_t* in, const uint64_t
         }
     }
     LZG_TRACE(ctx, st, "mf_walk done (%llu chains)", (unsigned long long)nchains);
-    int32_t* p_err = (int32_t*)(p_cnt + 1);
-    if (hipMemcpyAsync(p_err, w.err, sizeof(int), hipMemcpyDeviceToHost, st) != hipSuccess)
+    if (hipMemcpyAsync(p_cnt + 2, w.err, sizeof(int), hipMemcpyDeviceToHost, st) != hipSuccess)
         return ctx->fail(LZMA_E_DEVICE, "mf_walk: %s", hipGetErrorString(hipGetLastError()));
     return LZMA_OK;
 }
 
 // the walk's verdict, once the stream that launched it has passed its verdict copy
-int mf_walk_result(Ctx* ctx) {
-    const int32_t e = *(const int32_t*)(ctx->pin_mf.as<uint64_t>() + 1);
+int mf_walk_result(Ctx* ctx, int slot) {
+    const int32_t e = (int32_t)pin_slot(ctx, slot)[2];
     if (e == 3) return ctx->fail(LZMA_E_INTERNAL, "mf_walk: a tree link outside its bucket");
     if (e == 4) return ctx->fail(LZMA_E_INTERNAL, "mf_walk: a chain list entry out of range (index, extent, stream or member)");
     if (e) return LZMA_E_OVERFLOW;   // caller grows the overflow pool and retries
@@ -770,10 +784,11 @@ int mf_walk_result(Ctx* ctx) {
 
 int mf_back(Ctx* ctx, const Derived& d, const uint8_t* in, const uint64_t* d_offs, int nstreams, uint64_t total,
             bool wide_pairs, MfBuffers& w, hipStream_t st) {
-    int rc = mf_walk_launch(ctx, d, in, d_offs, nstreams, total, wide_pairs, w, st);
-    if (rc) return rc;
+    int rc;
+    if ((rc = mf_count_enqueue(ctx, w, nstreams, st, 0)) || (rc = mf_walk_launch(ctx, d, in, d_offs, nstreams, total, wide_pairs, w, st, 0)))
+        return rc;
     if (hipStreamSynchronize(st) != hipSuccess) return ctx->fail(LZMA_E_DEVICE, "mf_walk: %s", hipGetErrorString(hipGetLastError()));
-    return mf_walk_result(ctx);
+    return mf_walk_result(ctx, 0);
 }
 
 }  // namespace lzg

@@ -136,13 +136,18 @@ struct Ctx {
     // host-buffer entry points (lzma_enc_batch, lzma_dec_batch, lzma_match_lists): staging in HBM
     DevBuf io_in, io_out, io_pack, io_offs;
     HostBuf pin;        // encode-pass and pack staging (offsets, order, lengths, status)
-    HostBuf pin_mf;     // the match finder's chain-count readback
+    HostBuf pin_mf;     // the match finder's chain-count and walk-verdict readback, 32 bytes per slot
     std::string err;
     bool debug = getenv("LZMA_MI355X_DEBUG") != nullptr;   // phase trace on stderr (synchronises)
     uint64_t batch_bytes = 512ull << 20;
-    // persistent workspace arena (grown, never shrunk)
+    // persistent workspace arena (grown, never shrunk): the match finder's scratch, the
+    // parser's spill scratch, the decoder's and pack's workspace
     uint8_t* arena = nullptr;
     size_t arena_size = 0;
+    // an encode pass's buffers that live from its staging to its parse (input copy, pass
+    // arrays, match lists, overflow pool): slot 0 for the synchronous form, slots 0 / 1
+    // alternating for the split form, so one pass's walk can run beside the other's parse
+    DevBuf live[2];
     uint8_t* tmp = nullptr;     // cub temp storage
     size_t tmp_size = 0;
     uint64_t ovf_hint = 0;      // overflow pool slots per 1024 input bytes (0 = default; grows on retry)
@@ -158,12 +163,17 @@ struct Ctx {
     const Ctx* fence = nullptr;
     // split encode (lzma_enc_stage_dev -> lzma_enc_parse_dev_async -> lzma_enc_parse_dev_wait):
     // the staged pass, and the range coder in flight on the context's coder stream
-    EncPass* split_pass = nullptr;
-    int split_state = 0;                   // 0 idle, 1 staged, 2 parsed (coder in flight)
+    // the staged passes (at most two: the older one's parse may run beside the newer one's
+    // walk), oldest at split_head; split_state = how many are staged
+    EncPass* split_pass[2] = {nullptr, nullptr};
+    int split_head = 0;
+    int split_state = 0;
     int rc_pending = 0;                    // streams of the coder in flight
     hipEvent_t rc_done = nullptr, parse_done = nullptr;
-    hipEvent_t walk_done = nullptr;        // the split form: the staged walk's verdict copied to the host
+    hipEvent_t cnt_done[2] = {nullptr, nullptr};    // per slot: the chain count copied to the host
+    hipEvent_t walk_done[2] = {nullptr, nullptr};   // per slot: the walk's verdict copied to the host
     hipStream_t rc_stream = nullptr;       // created on first use
+    hipStream_t walk_stream = nullptr;     // a staged pass's walk beside the older pass's parse
     DevBuf split_recs, split_coder;        // the coder's records and per-stream arrays (apart from the arena)
     HostBuf pin_rc;                        // the coder's lengths and verdicts
     // timing
@@ -315,12 +325,15 @@ int mf_front(Ctx* ctx, const Derived& d, const uint8_t* in, const uint64_t* d_of
              bool wide_pairs, MfBuffers& w, hipStream_t st);
 int mf_back(Ctx* ctx, const Derived& d, const uint8_t* in, const uint64_t* d_offs, int nstreams, uint64_t total,
             bool wide_pairs, MfBuffers& w, hipStream_t st);
-// mf_back in two halves: the walk and its verdict's copy enqueued on st (one host round
-// trip sizes the grid), then the verdict once st has passed that copy (the split encode
-// checks it when the parse is enqueued, so the walk runs while the host does other work)
+// mf_back in pieces, per pinned slot (0 / 1): the chain count's copy to the host enqueued
+// on the match finder's stream (cnt_done[slot] behind it); the walk, sized from that
+// count (the host waits for cnt_done[slot] only), and its verdict's copy enqueued on st
+// (which may be another stream: the split encode runs a staged pass's walk beside the
+// older pass's parse); the verdict once st has passed that copy
+int mf_count_enqueue(Ctx* ctx, const MfBuffers& w, int nstreams, hipStream_t st, int slot);
 int mf_walk_launch(Ctx* ctx, const Derived& d, const uint8_t* in, const uint64_t* d_offs, int nstreams, uint64_t total,
-                   bool wide_pairs, MfBuffers& w, hipStream_t st);
-int mf_walk_result(Ctx* ctx);
+                   bool wide_pairs, MfBuffers& w, hipStream_t st, int slot);
+int mf_walk_result(Ctx* ctx, int slot);
 // sort.hip: stable per-stream radix sort by the low end_bit key bits
 int seg_radix_sort(Ctx* ctx, bool key64, const void* kin, const uint32_t* vin, void* kout, uint32_t* vout,
                    uint64_t* tmp_a, uint64_t* tmp_b, uint32_t* hist, uint64_t n, const uint64_t* d_offs, int nstreams,

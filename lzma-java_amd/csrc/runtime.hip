@@ -120,7 +120,9 @@ struct EncPass {
     int ns = 0;
     uint64_t in0 = 0, total = 0;
     bool wide = false, split = false;
-    bool walk_launched = false;   // the split form: the walk was enqueued by the staging
+    int slot = 0;                 // live buffers, pinned words and events of ctx (split form: 0 / 1)
+    const uint8_t* carved_arena = nullptr;   // ctx->arena when the shared buffers were carved
+    int walk_state = 0;           // the split form: 0 the walk not enqueued, 1 enqueued (walk_done[slot] behind it)
     size_t psz = 4;
     std::vector<uint64_t> offs, oofs, rofs;
     std::vector<uint32_t> order;
@@ -176,10 +178,12 @@ static void pass_plan(Ctx* ctx, EncPass& P, const Derived& d, const uint8_t* d_i
     for (int i = 0; i < ns; i++) P.rofs[i + 1] = P.rofs[i] + rc_record_bound(P.offs[i + 1] - P.offs[i]);
 }
 
-// The arena layout for the pass's current overflow pool. The sync form keeps the coder
-// records in the memory of the match finder's buffers (dead after the walk); the split
-// form keeps them, and the coder's own arrays, in separate allocations (Ctx::split_*)
-// that the next pass's match finder never touches.
+// The layout for the pass's current overflow pool. The pass's live buffers (input copy,
+// pass arrays, match lists, overflow pool, the parser's spill scratch: staging to parse)
+// come from live[P.slot]; the match finder's scratch from the shared arena. The sync
+// form keeps the coder records in the memory of the match finder's buffers (dead after
+// the walk); the split form keeps them, and the coder's own arrays, in separate
+// allocations (Ctx::split_*) that the next pass's match finder never touches.
 static int pass_carve(Ctx* ctx, EncPass& P) {
     const uint64_t T = P.total;
     const int ns = P.ns;
@@ -205,7 +209,7 @@ static int pass_carve(Ctx* ctx, EncPass& P) {
     }
     const size_t rec_bytes_all = P.rofs[ns] * 2;
     const size_t union_bytes = P.split ? p1_bytes : std::max<size_t>(p1_bytes, rec_bytes_all);
-    auto need = [&](Carver& c, EncPass& Q) {
+    auto need_live = [&](Carver& c, EncPass& Q) {
         Q.inpad = c.take<uint8_t>(T + 512);
         Q.d_offs = c.take<uint64_t>(ns + 1);
         Q.d_oofs = c.take<uint64_t>(ns + 1);
@@ -216,30 +220,41 @@ static int pass_carve(Ctx* ctx, EncPass& P) {
         Q.d_rofs = c.take<uint64_t>(ns + 1);
         Q.d_rlens = c.take<uint64_t>(ns);
         Q.d_seg = c.take<uint32_t>((size_t)ns * kRcSegs * kRcSegWords);
-        uint8_t* u = c.take<uint8_t>(union_bytes);
-        Q.d_recs = (uint16_t*)u;
-        Carver c1(u);
-        phase1(c1, Q.w);
         Q.w.pairs = (v4u32*)c.take<uint8_t>(T * rec_bytes(Q.wide));
         Q.w.ovf_off = c.take<uint32_t>(T);
         Q.w.ovf = c.take<uint8_t>(Q.ovf_cap * Q.psz);
         Q.w.ovf_cap = Q.ovf_cap;
         Q.w.ovf_used = c.take<unsigned long long>(1);
         Q.w.err = c.take<int>(1);
+        // the parser's spill scratch: the pass's own (in the split form the newer pass's
+        // walk runs beside this pass's parse, over the shared match-finder scratch)
         Q.d_scr = c.take<uint8_t>((size_t)Q.grid * Q.scr);
     };
+    auto need_shared = [&](Carver& c, EncPass& Q) {   // one pass's keys, sorts, chains and tree at a time
+        uint8_t* u = c.take<uint8_t>(union_bytes);
+        Q.d_recs = (uint16_t*)u;
+        Carver c1(u);
+        phase1(c1, Q.w);
+    };
     {
-        Carver probe(nullptr);
+        Carver pl(nullptr), ps(nullptr);
         EncPass Q;
         Q.wide = P.wide; Q.ovf_cap = P.ovf_cap; Q.psz = P.psz; Q.grid = P.grid; Q.scr = P.scr;
-        need(probe, Q);
-        // the split form's coder may still read its own allocations, never the arena; a
-        // reallocation still waits for it (the coder's records live apart, but not its caller)
-        if (probe.off + 4096 > ctx->arena_size && ctx->rc_pending) HIPCHK(hipEventSynchronize(ctx->rc_done));
-        if (!ctx->ensure_arena(probe.off + 4096)) return ctx->fail(LZMA_E_NOMEM, "device workspace %zu bytes", probe.off);
+        need_live(pl, Q);
+        need_shared(ps, Q);
+        DevBuf& L = ctx->live[P.slot];
+        if (pl.off + 4096 > L.n || ps.off + 4096 > ctx->arena_size) {
+            // a reallocation waits for everything that may still read the old buffers: the
+            // other staged pass's walk, the older pass's parse, the coder's caller
+            if (ctx->split_state || ctx->rc_pending) HIPCHK(hipDeviceSynchronize());
+            if (!L.ensure(pl.off + 4096)) return ctx->fail(LZMA_E_NOMEM, "device workspace %zu bytes", pl.off);
+            if (!ctx->ensure_arena(ps.off + 4096)) return ctx->fail(LZMA_E_NOMEM, "device workspace %zu bytes", ps.off);
+        }
     }
-    Carver c(ctx->arena);
-    need(c, P);
+    Carver cl(ctx->live[P.slot].as<uint8_t>()), cs(ctx->arena);
+    need_live(cl, P);
+    need_shared(cs, P);
+    P.carved_arena = ctx->arena;
     if (P.split) {
         // records apart from the match finder's buffers; the coder's per-stream arrays apart
         // from the pass arrays the next pass's staging rewrites
@@ -251,6 +266,15 @@ static int pass_carve(Ctx* ctx, EncPass& P) {
         P.d_recs = ctx->split_recs.as<uint16_t>();
     }
     return LZMA_OK;
+}
+
+// The split form: a pass's pointers into the context's shared allocations (the arena's
+// match-finder and parser scratch, the coder records) as of now. Another pass's staging
+// may have grown, and so moved, them since this pass was carved (it waited for every user
+// of the old ones first); the live buffers are the pass's own slot's and do not move.
+static int pass_refresh_shared(Ctx* ctx, EncPass& P) {
+    if (P.carved_arena == ctx->arena && P.d_recs == ctx->split_recs.as<uint16_t>()) return LZMA_OK;
+    return pass_carve(ctx, P);   // sizes unchanged: no reallocation, the live slot's layout is the same
 }
 
 // host arrays through pinned staging (see HostBuf): the pass's later host round trip
@@ -278,23 +302,35 @@ static int pass_stage(Ctx* ctx, EncPass& P, hipStream_t st) {
     return LZMA_OK;
 }
 
-// the walk; on a full overflow pool, grow it (4x, remembered by the context) and run the
-// pass's match finder again from the staging. Returns LZMA_OK or an error.
-// launched: the walk was already enqueued (the split form's staging), with walk_done
-// recorded behind its verdict copy.
-static int pass_mf_back(Ctx* ctx, EncPass& P, hipStream_t st, bool launched = false) {
+// the walk on st now (its chain count read back through P's pinned slot), then its verdict
+static int walk_now(Ctx* ctx, EncPass& P, hipStream_t st) {
+    int rc;
+    if ((rc = mf_count_enqueue(ctx, P.w, P.ns, st, P.slot)) ||
+        (rc = mf_walk_launch(ctx, P.d, P.inpad, P.d_offs, P.ns, P.total, P.wide, P.w, st, P.slot)))
+        return rc;
+    HIPCHK(hipStreamSynchronize(st));
+    return mf_walk_result(ctx, P.slot);
+}
+
+// the walk (or, split form, the verdict of the walk already enqueued: walk_state 1); on a
+// full overflow pool, grow it (4x, remembered by the context) and run the pass's match
+// finder again from the staging. Returns LZMA_OK or an error; *redone: the match finder
+// ran again (its scratch now holds this pass's buffers).
+static int pass_mf_back(Ctx* ctx, EncPass& P, hipStream_t st, bool* redone = nullptr) {
     for (int attempt = 0; attempt < 6; attempt++) {
         int rc;
-        if (launched) {
-            launched = false;
-            HIPCHK(hipEventSynchronize(ctx->walk_done));
-            rc = mf_walk_result(ctx);
-        } else rc = mf_back(ctx, P.d, P.inpad, P.d_offs, P.ns, P.total, P.wide, P.w, st);
+        if (P.walk_state == 1) {
+            P.walk_state = 0;
+            HIPCHK(hipEventSynchronize(ctx->walk_done[P.slot]));
+            rc = mf_walk_result(ctx, P.slot);
+        } else rc = walk_now(ctx, P, st);
         if (rc != LZMA_E_OVERFLOW) return rc;
         if (P.slots_per_k >= 1024) return ctx->fail(LZMA_E_INTERNAL, "overflow pool full at one slot per position");
         P.slots_per_k = std::min<uint64_t>(1024, P.slots_per_k * 4);
         ctx->ovf_hint = P.slots_per_k;
         P.ovf_cap = P.pool_cap(P.slots_per_k);
+        if (redone) *redone = true;
+        HIPCHK(hipDeviceSynchronize());   // rare: the staging below reuses pinned memory other copies may read
         if ((rc = pass_carve(ctx, P)) || (rc = pass_stage(ctx, P, st)) ||
             (rc = mf_front(ctx, P.d, P.inpad, P.d_offs, P.ns, P.total, P.wide, P.w, st)))
             return rc;
@@ -468,10 +504,15 @@ __global__ void coder_arrays_kernel(int ns, const uint64_t* rofs, const uint64_t
     }
 }
 
+// The split form holds up to two staged passes (slots 0 / 1 of the live buffers, pinned
+// words and events). Steady state, as bench.py calls it: stage(k + 1), then parse_async(k).
+// Batch k + 1's keys and sorts (which need LDS) then run on st before batch k's parser, and
+// its walk (no LDS, latency-bound) runs on the walk stream beside that parser; batch k + 2's
+// staging waits for it, as its match finder reuses the same scratch.
 static int enc_stage_dev(Ctx* ctx, const lzma_params* p, const uint8_t* d_in, const uint64_t* h_offs, int nstreams,
                          uint8_t* d_out, const uint64_t* h_out_offs, hipStream_t st) {
     if (ctx->dec_pending) return ctx->fail(LZMA_E_PARAM, "an asynchronous decode is in flight: lzma_dec_batch_dev_wait first");
-    if (ctx->split_state) return ctx->fail(LZMA_E_PARAM, "a batch is already staged: lzma_enc_parse_dev_async first");
+    if (ctx->split_state >= 2) return ctx->fail(LZMA_E_PARAM, "two batches are already staged: lzma_enc_parse_dev_async first");
     Derived d;
     if (derive(*p, d) != LZMA_OK) return ctx->fail(LZMA_E_PARAM, "invalid lzma_params");
     if (nstreams <= 0) return ctx->fail(LZMA_E_PARAM, "the split form needs at least one stream");
@@ -480,47 +521,86 @@ static int enc_stage_dev(Ctx* ctx, const lzma_params* p, const uint8_t* d_in, co
     const uint64_t pass_cap = std::min<uint64_t>(ctx->batch_bytes, (1ull << 31) - 1);
     if (nstreams > kMaxStreamsPerPass || (nstreams > 1 && h_offs[nstreams] - h_offs[0] > pass_cap))
         return ctx->fail(LZMA_E_PARAM, "the split form takes one pass: at most %d streams and batch_bytes of input", kMaxStreamsPerPass);
-    if (!ctx->split_pass) ctx->split_pass = new (std::nothrow) EncPass;
-    if (!ctx->split_pass) return ctx->fail(LZMA_E_NOMEM, "split pass");
-    EncPass& P = *ctx->split_pass;
+    // Alone, the batch takes the slot the last consumed batch had (its parse, still running,
+    // comes first on st, and a reallocation waits for it): a caller that never stages two
+    // batches uses one live slot. The second staged batch takes the other slot.
+    if (ctx->split_state == 0) ctx->split_head = (ctx->split_head + 1) % 2;
+    const int slot = (ctx->split_head + ctx->split_state) % 2;
+    for (int k = 0; k < 2; k++) {
+        if (!ctx->walk_done[k] && hipEventCreateWithFlags(&ctx->walk_done[k], hipEventDisableTiming) != hipSuccess)
+            return ctx->fail(LZMA_E_DEVICE, "walk event");
+    }
+    if (ctx->split_state == 1) {
+        // the older staged pass's walk reads the match-finder scratch this staging rewrites
+        EncPass& O = *ctx->split_pass[ctx->split_head];
+        if (O.walk_state == 0) {
+            if ((rc = mf_walk_launch(ctx, O.d, O.inpad, O.d_offs, O.ns, O.total, O.wide, O.w, st, O.slot))) return rc;
+            HIPCHK(hipEventRecord(ctx->walk_done[O.slot], st));
+            O.walk_state = 1;
+        } else HIPCHK(hipStreamWaitEvent(st, ctx->walk_done[O.slot], 0));
+    }
+    if (!ctx->split_pass[slot]) ctx->split_pass[slot] = new (std::nothrow) EncPass;
+    if (!ctx->split_pass[slot]) return ctx->fail(LZMA_E_NOMEM, "split pass");
+    EncPass& P = *ctx->split_pass[slot];
     P = EncPass();
     pass_plan(ctx, P, d, d_in, h_offs, 0, nstreams, d_out, h_out_offs, true);
-    if (!ctx->walk_done && hipEventCreateWithFlags(&ctx->walk_done, hipEventDisableTiming) != hipSuccess)
-        return ctx->fail(LZMA_E_DEVICE, "walk event");
+    P.slot = slot;
     if ((rc = pass_carve(ctx, P)) || (rc = pass_stage(ctx, P, st)) ||
-        (rc = mf_front(ctx, P.d, P.inpad, P.d_offs, P.ns, P.total, P.wide, P.w, st)))
+        (rc = mf_front(ctx, P.d, P.inpad, P.d_offs, P.ns, P.total, P.wide, P.w, st)) ||
+        (rc = mf_count_enqueue(ctx, P.w, P.ns, st, slot)))
         return rc;
-    // Without a parse fence, the walk too: it then runs as soon as the sorts are done
-    // (behind the previous batch's parser on st) instead of when the caller next enqueues a
-    // parse, after collecting the previous batch's coder. Its grid is sized by a host read
-    // of the chain count, so this call then waits for the work ahead of it on st. With a
-    // fence, the caller's decode is on the critical path and must not wait behind that: the
-    // walk stays in lzma_enc_parse_dev_async.
+    // Alone (nothing older staged) and without a parse fence, the walk too: it then runs as
+    // soon as the sorts are done instead of when the caller next enqueues a parse. Its grid
+    // is sized by a host read of the chain count, so this call then waits for the work ahead
+    // of it on st. With a fence, the caller's decode is on the critical path and must not
+    // wait behind that: the walk stays in lzma_enc_parse_dev_async.
     bool fenced;
     {
         std::lock_guard<std::mutex> g(g_ctx_lock);
         fenced = ctx->fence != nullptr;
     }
-    if (!fenced) {
-        if ((rc = mf_walk_launch(ctx, P.d, P.inpad, P.d_offs, P.ns, P.total, P.wide, P.w, st))) return rc;
-        HIPCHK(hipEventRecord(ctx->walk_done, st));
-        P.walk_launched = true;
+    if (ctx->split_state == 0 && !fenced) {
+        if ((rc = mf_walk_launch(ctx, P.d, P.inpad, P.d_offs, P.ns, P.total, P.wide, P.w, st, slot))) return rc;
+        HIPCHK(hipEventRecord(ctx->walk_done[slot], st));
+        P.walk_state = 1;
     }
-    ctx->split_state = 1;
+    ctx->split_state++;
     return LZMA_OK;
 }
 
 static int enc_parse_dev_async(Ctx* ctx, hipStream_t st) {
     if (!ctx->split_state) return ctx->fail(LZMA_E_PARAM, "nothing staged: lzma_enc_stage_dev first");
     if (ctx->rc_pending) return ctx->fail(LZMA_E_PARAM, "the previous batch's coder is in flight: lzma_enc_parse_dev_wait first");
-    EncPass& P = *ctx->split_pass;
-    ctx->split_state = 0;   // from here on the staged pass is consumed (or failed)
+    EncPass& P = *ctx->split_pass[ctx->split_head];
+    // from here on the oldest staged pass is consumed (or failed)
+    ctx->split_head = (ctx->split_head + 1) % 2;
+    ctx->split_state--;
+    EncPass* Q = ctx->split_state ? ctx->split_pass[ctx->split_head] : nullptr;   // the newer staged pass
     int rc;
-    if ((rc = pass_mf_back(ctx, P, st, P.walk_launched))) return rc;
+    bool redone = false;
+    if ((rc = pass_mf_back(ctx, P, st, &redone))) { ctx->split_state = 0; return rc; }
+    if (redone && Q) {   // P's match finder ran again over the scratch Q's staging had filled
+        if ((rc = pass_refresh_shared(ctx, *Q)) || (rc = pass_stage(ctx, *Q, st)) || (rc = mf_front(ctx, Q->d, Q->inpad, Q->d_offs, Q->ns, Q->total, Q->wide, Q->w, st)) ||
+            (rc = mf_count_enqueue(ctx, Q->w, Q->ns, st, Q->slot))) { ctx->split_state = 0; return rc; }
+        Q->walk_state = 0;
+    }
     if (exp_env("LZG_PROBE_WALK_ONLY")) return LZMA_OK;   // experiment build: concurrency probe (tools/overlap_probe.py)
-    if ((rc = pass_parse(ctx, P, st))) return rc;
+    if ((rc = pass_refresh_shared(ctx, P)) || (rc = pass_parse(ctx, P, st))) { ctx->split_state = 0; return rc; }
     if (!ctx->rc_stream && hipStreamCreateWithFlags(&ctx->rc_stream, hipStreamNonBlocking) != hipSuccess)
         return ctx->fail(LZMA_E_DEVICE, "coder stream");
+    // The newer staged pass's walk beside this parse, on the walk stream: launched after the
+    // parser (its waves are resident first; the walk's take the rest), once its sorts are
+    // done (its chain count sizes the grid), and before the coder is enqueued: HIP streams
+    // share hardware queues (GPU_MAX_HW_QUEUES), and a walk queued behind the coder (which
+    // waits for this parse) would run after it, with the caller's copies behind the walk.
+    if (Q && Q->walk_state == 0) {
+        if (!ctx->walk_stream && hipStreamCreateWithFlags(&ctx->walk_stream, hipStreamNonBlocking) != hipSuccess)
+            return ctx->fail(LZMA_E_DEVICE, "walk stream");
+        if ((rc = mf_walk_launch(ctx, Q->d, Q->inpad, Q->d_offs, Q->ns, Q->total, Q->wide, Q->w, ctx->walk_stream, Q->slot)))
+            return rc;
+        HIPCHK(hipEventRecord(ctx->walk_done[Q->slot], ctx->walk_stream));
+        Q->walk_state = 1;
+    }
     if (!ctx->parse_done && hipEventCreateWithFlags(&ctx->parse_done, hipEventDisableTiming) != hipSuccess)
         return ctx->fail(LZMA_E_DEVICE, "parse event");
     if (!ctx->rc_done && hipEventCreateWithFlags(&ctx->rc_done, hipEventDisableTiming) != hipSuccess)
@@ -780,12 +860,17 @@ void lzma_ctx_destroy(lzma_ctx* ctx) {
     if (ctx->dec_pending) hipEventSynchronize(ctx->dec_done);
     if (ctx->dec_done) hipEventDestroy(ctx->dec_done);
     if (ctx->rc_pending) hipEventSynchronize(ctx->rc_done);
-    if (ctx->split_state) hipDeviceSynchronize();   // a staged pass's match finder may still run
+    if (ctx->split_state) hipDeviceSynchronize();   // a staged pass's match finder or walk may still run
     if (ctx->rc_done) hipEventDestroy(ctx->rc_done);
     if (ctx->parse_done) hipEventDestroy(ctx->parse_done);
-    if (ctx->walk_done) hipEventDestroy(ctx->walk_done);
+    for (int k = 0; k < 2; k++) {
+        if (ctx->walk_done[k]) hipEventDestroy(ctx->walk_done[k]);
+        if (ctx->cnt_done[k]) hipEventDestroy(ctx->cnt_done[k]);
+        delete ctx->split_pass[k];
+        ctx->live[k].release();
+    }
     if (ctx->rc_stream) hipStreamDestroy(ctx->rc_stream);
-    delete ctx->split_pass;
+    if (ctx->walk_stream) hipStreamDestroy(ctx->walk_stream);
     ctx->split_recs.release();
     ctx->split_coder.release();
     ctx->pin_rc.release();

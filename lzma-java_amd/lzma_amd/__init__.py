@@ -331,20 +331,26 @@ class Context:
     # the range coder of one batch runs on the context's coder stream while the next
     # batch's match finder runs on the caller's stream
     def encode_stage_dev(self, d_in, offs: np.ndarray, p: Params, d_out, out_offs: np.ndarray, stream_ptr: int = 0) -> None:
-        """Stage a batch and enqueue its match finder's front; returns without waiting."""
+        """Stage a batch and enqueue its match finder's keys and sorts (at most two batches
+        staged: the newer one's walk then runs beside the older one's parse)."""
         n = len(offs) - 1
         offs = np.ascontiguousarray(offs, dtype=np.uint64)
         out_offs = np.ascontiguousarray(out_offs, dtype=np.uint64)
         self.check(lib().lzma_enc_stage_dev(self.h, ctypes.byref(p), _dptr(d_in), offs.ctypes.data, n, _dptr(d_out),
                                             out_offs.ctypes.data, ctypes.c_void_p(stream_ptr)))
-        self._staged_n = n
+        self._staged = getattr(self, "_staged", []) + [n]
 
     def encode_parse_dev_async(self, stream_ptr: int = 0) -> None:
-        """The staged batch's walk and parser on the caller's stream, its range coder on the
-        context's coder stream; returns without waiting for them."""
-        self.check(lib().lzma_enc_parse_dev_async(self.h, ctypes.c_void_p(stream_ptr)))
-        self._coder_n = getattr(self, "_staged_n", 0)
-        self._staged_n = 0
+        """The oldest staged batch's walk and parser on the caller's stream, its range coder
+        on the context's coder stream; returns without waiting for them."""
+        rc = lib().lzma_enc_parse_dev_async(self.h, ctypes.c_void_p(stream_ptr))
+        staged = getattr(self, "_staged", [])
+        if rc != LZMA_OK:
+            if rc != LZMA_E_PARAM:   # a refusal consumes nothing; a failed parse drops every staged batch
+                self._staged = []
+            self.check(rc)
+        self._coder_n = staged[0] if staged else 0
+        self._staged = staged[1:]
 
     def encode_parse_dev_wait(self) -> np.ndarray:
         """Wait for the range coder; the encoded lengths."""

@@ -96,7 +96,7 @@ def _split_worker(q):
         offs[1:] = np.cumsum([len(s) for s in streams])
         caps = np.zeros(len(streams) + 1, dtype=np.uint64)
         caps[1:] = np.cumsum([lzma_amd.enc_bound(len(s)) for s in streams])
-        outs = [np.zeros(int(caps[-1]) + 1, dtype=np.uint8) for _ in range(2)]
+        outs = [np.zeros(int(caps[-1]) + 1, dtype=np.uint8) for _ in range(3)]
 
         def got(buf, lens):
             return [buf[int(caps[i]):int(caps[i]) + int(lens[i])].tobytes() for i in range(len(streams))]
@@ -111,9 +111,8 @@ def _split_worker(q):
         r = {}
         r["parse_before_stage"] = refused(lambda: ctx.encode_parse_dev_async())
         r["wait_before_parse"] = refused(lambda: ctx.encode_parse_dev_wait())
-        # the pipelined order: stage A, parse A, stage B (A's coder in flight), wait A, parse B, wait B
+        # the round-4 order: stage A, parse A, stage B (A's coder in flight), wait A, parse B, wait B
         ctx.encode_stage_dev(src.ctypes.data, offs, p, outs[0].ctypes.data, caps)
-        r["stage_twice"] = refused(lambda: ctx.encode_stage_dev(src.ctypes.data, offs, p, outs[0].ctypes.data, caps))
         r["sync_while_staged"] = refused(lambda: ctx.encode_batch_dev(src.ctypes.data, offs, p, outs[1].ctypes.data, caps))
         r["pack_while_staged"] = refused(lambda: ctx.pack_dev(outs[0].ctypes.data, caps, np.ones(len(streams), np.uint64),
                                                               outs[1].ctypes.data))
@@ -125,6 +124,35 @@ def _split_worker(q):
         lens_b = ctx.encode_parse_dev_wait()
         r["a_equal"] = got(outs[0], lens_a) == ref
         r["b_equal"] = got(outs[1], lens_b) == ref
+        # the round-5 order (bench.py): the next batch staged before the parse, so its walk
+        # runs beside it: stage A, stage B, parse A (B's walk), wait A, stage C, parse B
+        # (C's walk), wait B, parse C, wait C; a third staged batch is refused
+        # Batches of different layouts (a larger second batch grows the shared scratch while
+        # the first one is staged: its pointers there are refreshed before its parse).
+        def batch(nbytes, cut):
+            x = np.frombuffer(data[:nbytes] + b"\0" * 16, dtype=np.uint8).copy()
+            ss = [data[i:min(i + cut, nbytes)] for i in range(0, nbytes, cut)]
+            o = np.zeros(len(ss) + 1, dtype=np.uint64)
+            o[1:] = np.cumsum([len(t) for t in ss])
+            c = np.zeros(len(ss) + 1, dtype=np.uint64)
+            c[1:] = np.cumsum([lzma_amd.enc_bound(len(t)) for t in ss])
+            return x, o, c, np.zeros(int(c[-1]) + 1, dtype=np.uint8), ss
+        bs = [batch(4000, 1500), batch(len(data), 2500), batch(9000, 4000)]
+        stage = lambda b: ctx.encode_stage_dev(b[0].ctypes.data, b[1], p, b[3].ctypes.data, b[2])
+        stage(bs[0])
+        stage(bs[1])
+        r["stage_thrice"] = refused(lambda: stage(bs[2]))
+        ctx.encode_parse_dev_async()
+        lens = [ctx.encode_parse_dev_wait()]
+        stage(bs[2])
+        ctx.encode_parse_dev_async()
+        lens.append(ctx.encode_parse_dev_wait())
+        ctx.encode_parse_dev_async()
+        lens.append(ctx.encode_parse_dev_wait())
+        for k, (b, ln) in enumerate(zip(bs, lens)):
+            x, o, c, out, ss = b
+            r["next_staged_%d_equal" % k] = [out[int(c[i]):int(c[i]) + int(ln[i])].tobytes() for i in range(len(ss))] == \
+                ctx.encode_batch(ss, p)
         # the synchronous entry points work again once the coder is collected
         r["sync_after"] = ctx.encode_batch(streams[:2], p) == ref[:2]
         # one pass only: a batch above batch_bytes is refused

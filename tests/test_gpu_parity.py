@@ -270,6 +270,61 @@ def test_gpu_split_encode_pipelined_order():
 
 
 @pytest.mark.parametrize("fenced", [False, True])
+def test_gpu_split_encode_next_staged_before_parse(fenced):
+    """The round-5 pipelined order (bench.py): batch k + 1 staged before batch k's parse, so
+    its keys and sorts run ahead of that parser and its walk on the context's walk stream
+    beside it, in two live-buffer slots: stage A, stage B, parse A, wait A, stage C (A's slot,
+    after B's walk), parse B, wait B, parse C, wait C. Three batches of different layouts
+    (stream counts, ragged sizes, BENCH / TEXT), every stream byte-equal to the oracle's
+    Encoder.Code; a third staged batch is refused. Fenced (a decoder context as the parse
+    fence) and not."""
+    torch = pytest.importorskip("torch")
+    c = lzma_amd.Context(0)
+    dec = lzma_amd.Context(0) if fenced else None
+    if fenced:
+        c.set_parse_fence(dec)
+    try:
+        p = lzma_amd.make_params(dict_size=1 << 26, fb=32)
+        st = torch.cuda.current_stream().cuda_stream
+        rng = np.random.default_rng(77)
+        batches = []
+        for size, n, gen in ((1 << 20, 8, lzma_amd.bench_generate), (3 << 20, 13, lzma_amd.text_generate),
+                             (2 << 20, 5, lzma_amd.bench_generate)):
+            x = gen(size)
+            cuts = np.sort(rng.integers(1, size, n - 1))
+            offs = np.concatenate([[0], cuts, [size]]).astype(np.uint64)
+            caps = [lzma_amd.enc_bound(int(offs[i + 1] - offs[i])) for i in range(n)]
+            oo = np.zeros(n + 1, dtype=np.uint64)
+            oo[1:] = np.cumsum(caps)
+            batches.append((x, offs, oo, torch.from_numpy(x).cuda(),
+                            torch.empty(int(oo[-1]), dtype=torch.uint8, device="cuda")))
+        stage = lambda b: c.encode_stage_dev(b[3], b[1], p, b[4], b[2], st)
+        stage(batches[0])
+        stage(batches[1])
+        with pytest.raises(lzma_amd.LzmaError):
+            stage(batches[2])   # two are staged already
+        c.encode_parse_dev_async(st)
+        lens = [c.encode_parse_dev_wait()]
+        stage(batches[2])
+        c.encode_parse_dev_async(st)
+        lens.append(c.encode_parse_dev_wait())
+        c.encode_parse_dev_async(st)
+        lens.append(c.encode_parse_dev_wait())
+        torch.cuda.synchronize()
+        for (x, offs, oo, _, buf), ln in zip(batches, lens):
+            n = len(offs) - 1
+            h = buf.cpu().numpy()
+            refs = orc.encode_many([x[int(offs[i]):int(offs[i + 1])].tobytes() for i in range(n)], _oparams(p))
+            for i in range(n):
+                assert h[int(oo[i]):int(oo[i] + ln[i])].tobytes() == refs[i], (n, i)
+    finally:
+        if fenced:
+            c.set_parse_fence(None)
+            dec.close()
+        c.close()
+
+
+@pytest.mark.parametrize("fenced", [False, True])
 def test_gpu_split_encode_heterogeneous_batches(fenced):
     """The split encode with batches of DIFFERENT layouts: batch B has more
     streams, ragged sizes and a larger total than batch A, and is staged -- its offsets,
