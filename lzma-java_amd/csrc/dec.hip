@@ -500,7 +500,8 @@ constexpr int kDecLitpMaxStreams = 2048;
 template <int PBS>
 static void launch_dec(const DecArgs& a, int grid, size_t lds, hipStream_t st) {
     (void)lds;   // static LDS (kDecLdsBytes)
-    if (a.lc + a.lp <= kDecLitpBits && grid <= kDecLitpMaxStreams)
+    static const int litp_max = exp_env("LZG_DEC_LITP_MAX") ? atoi(exp_env("LZG_DEC_LITP_MAX")) : kDecLitpMaxStreams;   // experiment build
+    if (a.lc + a.lp <= kDecLitpBits && grid <= litp_max)
         hipLaunchKernelGGL((dec_kernel<PBS, true>), dim3(grid), dim3(kWave), 0, st, a);
     else hipLaunchKernelGGL((dec_kernel<PBS, false>), dim3(grid), dim3(kWave), 0, st, a);
 }

@@ -29,7 +29,10 @@ namespace lzg {
 constexpr int kSW = 64;                  // ballot group (hardware wave) size
 constexpr int kSortThreads = 256;
 constexpr int kSortWaves = kSortThreads / kSW;
-constexpr int kSortRounds = 8;           // rounds of kSW items per wave and tile
+#ifndef LZG_SORT_ROUNDS
+#define LZG_SORT_ROUNDS 8
+#endif
+constexpr int kSortRounds = LZG_SORT_ROUNDS;   // rounds of kSW items per wave and tile
 constexpr int kSortTile = kSortThreads * kSortRounds;
 constexpr int kMaxPasses = 4;
 
