@@ -151,18 +151,21 @@ struct Enc {
                          E_MID = PL::MID, E_HIGH = PL::HIGH, E_COUNT = PL::COUNT;
     uint32_t lane_v;          // threadIdx.x: read through lane_id()
     // The lane index. In the kernels whose literal coders live in HBM (many streams per CU:
-    // 16 per CU, a 128-VGPR budget) it is opaque to the optimizer at every use: otherwise LICM
-    // hoists every lane-derived value (lane + c, lane == c, 7 - (lane & 7), ...) of the whole
-    // kernel to its entry, where hundreds of them hold VGPRs and SGPR pairs for the kernel's
-    // lifetime and spilled to scratch (128 VGPRs + scratch -> 56 VGPRs, none; 4096 streams
-    // 569 -> 537 ms). With the literal coders in LDS (few streams per CU, the budget the LDS
-    // leaves is larger) the hoisted values fit, and recomputing them cost one stream 5 %.
-    FI uint32_t lane_id() const {
-        uint32_t l = lane_v;
+    // 16 per CU, a 128-VGPR budget) it is made opaque to the optimizer once per coded symbol
+    // and once per forward position (refresh_lane): otherwise LICM hoists every lane-derived
+    // value (lane + c, lane == c, 7 - (lane & 7), ...) of the whole kernel to its entry, where
+    // hundreds of them hold VGPRs and SGPR pairs for the kernel's lifetime and spilled to
+    // scratch (128 VGPRs + scratch -> 56 VGPRs, none; 4096 streams 569 -> 537 ms). Opaque at
+    // every use instead, each use recomputed its value (432 instructions per byte); once per
+    // iteration, the values are shared within the iteration: 60 VGPRs, 4096 streams
+    // 532 -> 522 ms (profiles/r05/ab_parse_lane_refresh.jsonl). With the literal coders in LDS
+    // (few streams per CU, the budget the LDS leaves is larger) the hoisted values fit, and
+    // recomputing them cost one stream 5 %.
+    FI uint32_t lane_id() const { return lane_v; }
+    FI void refresh_lane() {
 #if LZG_WAVE == 64
-        if constexpr (!LIT_LDS) asm volatile("" : "+v"(l));
+        if constexpr (!LIT_LDS) asm volatile("" : "+v"(lane_v));
 #endif
-        return l;
     }
     // ---- LDS
     uint16_t* pp;             // ProbPrices [512]
@@ -1416,6 +1419,7 @@ struct Enc {
         DBG(5, len_end);
         for (;;) {
             cur++;
+            refresh_lane();
             DBG(6, cur);
             if (bad) { *back_res = -1; return 1; }
             if (cur == len_end) return backward(back_res, cur);
@@ -1548,6 +1552,7 @@ struct Enc {
         DBG(1, 6);
         for (;;) {
             int32_t back;
+            refresh_lane();
             DBG(2, now_pos);
             DBG(3, mfpos);
 #ifdef LZG_PROF
