@@ -209,6 +209,7 @@ def run_pass(args, D, p, ctxs, strong, rank, world, dist):
     cap_offs = np.zeros(n + 1, dtype=np.uint64)
     cap_offs[1:] = np.cumsum(caps)
     d_comp = torch.empty(int(cap_offs[-1]) + 1, dtype=torch.uint8, device=D.dev)
+    d_comps = [d_comp]   # the unfenced split schedule codes batch j into d_comps[j % 2]
     d_packs = [torch.empty(int(cap_offs[-1]) + 1, dtype=torch.uint8, device=D.dev) for _ in range(2)]
     d_dec = torch.empty(my_size + 1, dtype=torch.uint8, device=D.dev)
     out_sizes = lens_in.astype(np.int64)
@@ -222,6 +223,9 @@ def run_pass(args, D, p, ctxs, strong, rank, world, dist):
     fence = overlap and n > 8 * D.cus()
     if fence:
         ctx.set_parse_fence(ctx_dec)
+    lagged = overlap and args.pipeline == "split" and not fence
+    if lagged:
+        d_comps.append(torch.empty_like(d_comp))
 
     def check_dec(dlens, dstat):
         state["dec_ok"] &= bool((dstat == 0).all()) and bool((dlens == out_sizes).all())
@@ -258,18 +262,6 @@ def run_pass(args, D, p, ctxs, strong, rank, world, dist):
             if ahead:
                 stage()
             lens = ctx.encode_parse_dev_wait()
-        elif overlap and args.pipeline == "split":
-            # <= 8 streams per CU: two batches staged. Step k+1's keys and sorts ran on st
-            # ahead of step k's parser, its walk runs on the encoder context's walk stream
-            # beside that parser (the walk needs no LDS); step k+2's keys and sorts follow the
-            # parser on st at once (not after the host has collected step k's coder)
-            while state.get("staged", 0) < 1 + min(ahead, 1):
-                stage()
-            ctx.encode_parse_dev_async(st)
-            state["staged"] -= 1
-            if ahead >= 2:
-                stage()
-            lens = ctx.encode_parse_dev_wait()
         if overlap and args.pipeline == "split":
             join()   # step k-1's decode (fenced: done, step k's parser waited for it)
             pk = ctx_dec.pack_dev(d_comp, cap_offs, lens, buf, st_dec)   # synchronous: buf is complete
@@ -285,6 +277,41 @@ def run_pass(args, D, p, ctxs, strong, rank, world, dist):
         join()
         decode(buf, pk)
 
+    def finish(k, lens, t0):   # a lagged step's tail: pack + gather + decode of batch k
+        buf = d_packs[k % 2]
+        join()   # batch k-1's decode
+        pk = ctx_dec.pack_dev(d_comps[k % 2], cap_offs, lens, buf, st_dec)   # synchronous: buf is complete
+        if dist:
+            g, all_lens, counts = lzdist.gather_streams(buf, lens, dst=0)
+            state["gathered"] = None if g is None else (g, all_lens, counts)
+        state["lens"], state["pk"], state["buf"] = lens, pk, buf
+        state["t_enc"] = state.get("t_enc", 0.0) + (time.perf_counter() - t0)
+        decode(buf, pk)
+
+    def loop_lagged(nsteps):
+        # <= 8 streams per CU, no parse fence: two batches staged and two range coders in
+        # flight (one per live slot). On st: parser k, then batch k+2's keys and sorts, then
+        # parser k+1 at once (enqueued before the host collects coder k, which runs beside
+        # them); batch k+1's walk runs on the encoder context's walk stream beside parser k,
+        # step k's pack + decode beside parser k+1. Batch j codes into d_comps[j % 2].
+        def stage_j(j):
+            ctx.encode_stage_dev(d_in, offs, p, d_comps[j % 2], cap_offs, st)
+        if nsteps == 0:
+            return
+        stage_j(0)
+        if nsteps > 1:
+            stage_j(1)
+        ctx.encode_parse_dev_async(st)
+        if nsteps > 2:
+            stage_j(2)
+        for k in range(nsteps):
+            t0 = time.perf_counter()
+            if k + 1 < nsteps:
+                ctx.encode_parse_dev_async(st)
+                if k + 3 < nsteps:
+                    stage_j(k + 3)
+            finish(k, ctx.encode_parse_dev_wait(), t0)
+
     def barrier():
         if dist:
             torch.distributed.barrier()
@@ -292,8 +319,11 @@ def run_pass(args, D, p, ctxs, strong, rank, world, dist):
 
     # every step stages the next one inside its own time; the last step of each loop
     # stages nothing, so the timed loop holds exactly its own steps' work
-    for k in range(args.warmup):
-        step(k, args.warmup - 1 - k)
+    if lagged:
+        loop_lagged(args.warmup)
+    else:
+        for k in range(args.warmup):
+            step(k, args.warmup - 1 - k)
     join()
     for c in (ctx, ctx_dec):
         c.set_timing(True)
@@ -301,8 +331,11 @@ def run_pass(args, D, p, ctxs, strong, rank, world, dist):
     state["t_enc"] = state["t_dec"] = 0.0
     barrier()
     t0 = time.perf_counter()
-    for k in range(args.steps):
-        step(k, args.steps - 1 - k)
+    if lagged:
+        loop_lagged(args.steps)
+    else:
+        for k in range(args.steps):
+            step(k, args.steps - 1 - k)
     join()
     barrier()
     elapsed = time.perf_counter() - t0

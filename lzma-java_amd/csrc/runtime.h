@@ -168,14 +168,16 @@ struct Ctx {
     EncPass* split_pass[2] = {nullptr, nullptr};
     int split_head = 0;
     int split_state = 0;
-    int rc_pending = 0;                    // streams of the coder in flight
-    hipEvent_t rc_done = nullptr, parse_done = nullptr;
+    // range coders in flight (at most two, one per slot, oldest first): rc_pending = how many
+    int rc_pending = 0;
+    int rc_slot[2] = {0, 0}, rc_ns[2] = {0, 0};
+    hipEvent_t rc_done[2] = {nullptr, nullptr}, parse_done[2] = {nullptr, nullptr};
     hipEvent_t cnt_done[2] = {nullptr, nullptr};    // per slot: the chain count copied to the host
     hipEvent_t walk_done[2] = {nullptr, nullptr};   // per slot: the walk's verdict copied to the host
     hipStream_t rc_stream = nullptr;       // created on first use
     hipStream_t walk_stream = nullptr;     // a staged pass's walk beside the older pass's parse
-    DevBuf split_recs, split_coder;        // the coder's records and per-stream arrays (apart from the arena)
-    HostBuf pin_rc;                        // the coder's lengths and verdicts
+    DevBuf split_recs[2], split_coder[2];  // per slot: the coder's records and per-stream arrays (apart from the arena)
+    HostBuf pin_rc[2];                     // per slot: the coder's lengths and verdicts, written by the device
     // timing
     bool timing = false;
     struct Pending { std::string name; hipEvent_t a, b; };

@@ -259,11 +259,12 @@ static int pass_carve(Ctx* ctx, EncPass& P) {
         // records apart from the match finder's buffers; the coder's per-stream arrays apart
         // from the pass arrays the next pass's staging rewrites
         const size_t coder_bytes = (size_t)(ns + 1) * 8 * 4 + (size_t)ns * 8 + (size_t)ns * kRcSegs * kRcSegWords * 4 + 4096;
-        if ((rec_bytes_all > ctx->split_recs.n || coder_bytes > ctx->split_coder.n) && ctx->rc_pending)
-            HIPCHK(hipEventSynchronize(ctx->rc_done));
-        if (!ctx->split_recs.ensure(std::max<size_t>(rec_bytes_all, 256)) || !ctx->split_coder.ensure(coder_bytes))
+        DevBuf &R = ctx->split_recs[P.slot], &C = ctx->split_coder[P.slot];
+        if (rec_bytes_all > R.n || coder_bytes > C.n)   // a reallocation waits for the coders in flight
+            for (int q = 0; q < ctx->rc_pending; q++) HIPCHK(hipEventSynchronize(ctx->rc_done[ctx->rc_slot[q]]));
+        if (!R.ensure(std::max<size_t>(rec_bytes_all, 256)) || !C.ensure(coder_bytes))
             return ctx->fail(LZMA_E_NOMEM, "coder records %zu bytes", rec_bytes_all);
-        P.d_recs = ctx->split_recs.as<uint16_t>();
+        P.d_recs = R.as<uint16_t>();
     }
     return LZMA_OK;
 }
@@ -273,7 +274,7 @@ static int pass_carve(Ctx* ctx, EncPass& P) {
 // may have grown, and so moved, them since this pass was carved (it waited for every user
 // of the old ones first); the live buffers are the pass's own slot's and do not move.
 static int pass_refresh_shared(Ctx* ctx, EncPass& P) {
-    if (P.carved_arena == ctx->arena && P.d_recs == ctx->split_recs.as<uint16_t>()) return LZMA_OK;
+    if (P.carved_arena == ctx->arena && P.d_recs == ctx->split_recs[P.slot].as<uint16_t>()) return LZMA_OK;
     return pass_carve(ctx, P);   // sizes unchanged: no reallocation, the live slot's layout is the same
 }
 
@@ -486,8 +487,8 @@ struct CoderArrays {
     uint32_t *order, *seg;
     int32_t* status;
 };
-static CoderArrays coder_arrays(Ctx* ctx, int ns) {
-    Carver c(ctx->split_coder.as<uint8_t>());
+static CoderArrays coder_arrays(Ctx* ctx, int slot, int ns) {
+    Carver c(ctx->split_coder[slot].as<uint8_t>());
     CoderArrays r;
     r.rofs = c.take<uint64_t>(ns + 1); r.oofs = c.take<uint64_t>(ns + 1);
     r.rlens = c.take<uint64_t>(ns); r.lens = c.take<uint64_t>(ns);
@@ -509,6 +510,16 @@ __global__ void coder_arrays_kernel(int ns, const uint64_t* rofs, const uint64_t
 // Batch k + 1's keys and sorts (which need LDS) then run on st before batch k's parser, and
 // its walk (no LDS, latency-bound) runs on the walk stream beside that parser; batch k + 2's
 // staging waits for it, as its match finder reuses the same scratch.
+// the coder's per-stream lengths and verdicts into pinned host memory, on the coder stream
+// behind the coder (a kernel, not a copy: a device-to-host copy queued behind the coder
+// would hold a copy engine that other streams' copies need)
+__global__ void coder_out_kernel(int ns, const uint64_t* lens, const int32_t* status, uint64_t* h_lens, int32_t* h_status) {
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < ns; i += gridDim.x * blockDim.x) {
+        h_lens[i] = lens[i];
+        h_status[i] = status[i];
+    }
+}
+
 static int enc_stage_dev(Ctx* ctx, const lzma_params* p, const uint8_t* d_in, const uint64_t* h_offs, int nstreams,
                          uint8_t* d_out, const uint64_t* h_out_offs, hipStream_t st) {
     if (ctx->dec_pending) return ctx->fail(LZMA_E_PARAM, "an asynchronous decode is in flight: lzma_dec_batch_dev_wait first");
@@ -570,7 +581,7 @@ static int enc_stage_dev(Ctx* ctx, const lzma_params* p, const uint8_t* d_in, co
 
 static int enc_parse_dev_async(Ctx* ctx, hipStream_t st) {
     if (!ctx->split_state) return ctx->fail(LZMA_E_PARAM, "nothing staged: lzma_enc_stage_dev first");
-    if (ctx->rc_pending) return ctx->fail(LZMA_E_PARAM, "the previous batch's coder is in flight: lzma_enc_parse_dev_wait first");
+    if (ctx->rc_pending >= 2) return ctx->fail(LZMA_E_PARAM, "two coders are in flight: lzma_enc_parse_dev_wait first");
     EncPass& P = *ctx->split_pass[ctx->split_head];
     // from here on the oldest staged pass is consumed (or failed)
     ctx->split_head = (ctx->split_head + 1) % 2;
@@ -585,6 +596,10 @@ static int enc_parse_dev_async(Ctx* ctx, hipStream_t st) {
         Q->walk_state = 0;
     }
     if (exp_env("LZG_PROBE_WALK_ONLY")) return LZMA_OK;   // experiment build: concurrency probe (tools/overlap_probe.py)
+    // a coder still in flight on P's slot (its records, its coder arrays): P's parser and the
+    // copy of P's coder arrays wait for it on the device
+    for (int q = 0; q < ctx->rc_pending; q++)
+        if (ctx->rc_slot[q] == P.slot) HIPCHK(hipStreamWaitEvent(st, ctx->rc_done[P.slot], 0));
     if ((rc = pass_refresh_shared(ctx, P)) || (rc = pass_parse(ctx, P, st))) { ctx->split_state = 0; return rc; }
     if (!ctx->rc_stream && hipStreamCreateWithFlags(&ctx->rc_stream, hipStreamNonBlocking) != hipSuccess)
         return ctx->fail(LZMA_E_DEVICE, "coder stream");
@@ -601,40 +616,46 @@ static int enc_parse_dev_async(Ctx* ctx, hipStream_t st) {
         HIPCHK(hipEventRecord(ctx->walk_done[Q->slot], ctx->walk_stream));
         Q->walk_state = 1;
     }
-    if (!ctx->parse_done && hipEventCreateWithFlags(&ctx->parse_done, hipEventDisableTiming) != hipSuccess)
+    const int ps = P.slot;
+    if (!ctx->parse_done[ps] && hipEventCreateWithFlags(&ctx->parse_done[ps], hipEventDisableTiming) != hipSuccess)
         return ctx->fail(LZMA_E_DEVICE, "parse event");
-    if (!ctx->rc_done && hipEventCreateWithFlags(&ctx->rc_done, hipEventDisableTiming) != hipSuccess)
+    if (!ctx->rc_done[ps] && hipEventCreateWithFlags(&ctx->rc_done[ps], hipEventDisableTiming) != hipSuccess)
         return ctx->fail(LZMA_E_DEVICE, "coder event");
     // The copy of the pass arrays runs on the caller's stream, ahead of parse_done: a
     // later lzma_enc_stage_dev on that stream rewrites the pass arrays (a new batch's
     // offsets, order, status), and stream order keeps that behind this copy. Only the
     // coder itself runs on the coder stream.
-    const CoderArrays ca = coder_arrays(ctx, P.ns);
+    const CoderArrays ca = coder_arrays(ctx, ps, P.ns);
     hipLaunchKernelGGL(coder_arrays_kernel, dim3((P.ns + 256) / 256), dim3(256), 0, st, P.ns, P.d_rofs, P.d_rlens,
                        P.d_oofs, P.d_lens, P.d_order, P.d_status, ca);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord(ctx->parse_done, st));
-    HIPCHK(hipStreamWaitEvent(ctx->rc_stream, ctx->parse_done, 0));
+    HIPCHK(hipEventRecord(ctx->parse_done[ps], st));
+    HIPCHK(hipStreamWaitEvent(ctx->rc_stream, ctx->parse_done[ps], 0));
     if ((rc = pass_rc(ctx, P, ca.rofs, ca.rlens, ca.order, ca.status, ca.oofs, ca.lens, ca.seg, ctx->rc_stream))) return rc;
-    HIPCHK(hipEventRecord(ctx->rc_done, ctx->rc_stream));
-    ctx->rc_pending = P.ns;
+    if ((size_t)P.ns * 12 + 16 > ctx->pin_rc[ps].n)   // a reallocation waits for a coder still writing there
+        for (int q = 0; q < ctx->rc_pending; q++)
+            if (ctx->rc_slot[q] == ps) HIPCHK(hipEventSynchronize(ctx->rc_done[ps]));
+    if (!ctx->pin_rc[ps].ensure((size_t)P.ns * 12 + 16)) return ctx->fail(LZMA_E_NOMEM, "pinned staging");
+    uint64_t* h_lens = ctx->pin_rc[ps].as<uint64_t>();
+    hipLaunchKernelGGL(coder_out_kernel, dim3((P.ns + 255) / 256), dim3(256), 0, ctx->rc_stream, P.ns, ca.lens, ca.status,
+                       h_lens, (int32_t*)(h_lens + P.ns));
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(ctx->rc_done[ps], ctx->rc_stream));
+    ctx->rc_slot[ctx->rc_pending] = ps;
+    ctx->rc_ns[ctx->rc_pending] = P.ns;
+    ctx->rc_pending++;
     return LZMA_OK;
 }
 
 static int enc_parse_dev_wait(Ctx* ctx, uint64_t* h_out_lens) {
     if (!ctx->rc_pending) return ctx->fail(LZMA_E_PARAM, "no coder in flight: lzma_enc_parse_dev_async first");
-    const int ns = ctx->rc_pending;
-    ctx->rc_pending = 0;
-    // no device-to-host copy waits behind the coder (it would hold the copy engine): they
-    // are queued once it is done
-    HIPCHK(hipEventSynchronize(ctx->rc_done));
-    if (!ctx->pin_rc.ensure((size_t)ns * 12 + 16)) return ctx->fail(LZMA_E_NOMEM, "pinned staging");
-    uint64_t* p_lens = ctx->pin_rc.as<uint64_t>();
-    int32_t* p_status = (int32_t*)(p_lens + ns);
-    const CoderArrays ca = coder_arrays(ctx, ns);
-    HIPCHK(hipMemcpyAsync(p_lens, ca.lens, (size_t)ns * 8, hipMemcpyDeviceToHost, ctx->rc_stream));
-    HIPCHK(hipMemcpyAsync(p_status, ca.status, (size_t)ns * 4, hipMemcpyDeviceToHost, ctx->rc_stream));
-    HIPCHK(hipStreamSynchronize(ctx->rc_stream));
+    const int slot = ctx->rc_slot[0], ns = ctx->rc_ns[0];   // the oldest coder
+    ctx->rc_slot[0] = ctx->rc_slot[1];
+    ctx->rc_ns[0] = ctx->rc_ns[1];
+    ctx->rc_pending--;
+    HIPCHK(hipEventSynchronize(ctx->rc_done[slot]));   // coder_out_kernel has written the pinned words
+    const uint64_t* p_lens = ctx->pin_rc[slot].as<uint64_t>();
+    const int32_t* p_status = (const int32_t*)(p_lens + ns);
     memcpy(h_out_lens, p_lens, (size_t)ns * 8);
     for (int i = 0; i < ns; i++)
         if (p_status[i] != LZMA_OK)
@@ -859,11 +880,14 @@ void lzma_ctx_destroy(lzma_ctx* ctx) {
     for (auto e : ctx->free_events) hipEventDestroy(e);
     if (ctx->dec_pending) hipEventSynchronize(ctx->dec_done);
     if (ctx->dec_done) hipEventDestroy(ctx->dec_done);
-    if (ctx->rc_pending) hipEventSynchronize(ctx->rc_done);
+    for (int q = 0; q < ctx->rc_pending; q++) hipEventSynchronize(ctx->rc_done[ctx->rc_slot[q]]);
     if (ctx->split_state) hipDeviceSynchronize();   // a staged pass's match finder or walk may still run
-    if (ctx->rc_done) hipEventDestroy(ctx->rc_done);
-    if (ctx->parse_done) hipEventDestroy(ctx->parse_done);
     for (int k = 0; k < 2; k++) {
+        if (ctx->rc_done[k]) hipEventDestroy(ctx->rc_done[k]);
+        if (ctx->parse_done[k]) hipEventDestroy(ctx->parse_done[k]);
+        ctx->split_recs[k].release();
+        ctx->split_coder[k].release();
+        ctx->pin_rc[k].release();
         if (ctx->walk_done[k]) hipEventDestroy(ctx->walk_done[k]);
         if (ctx->cnt_done[k]) hipEventDestroy(ctx->cnt_done[k]);
         delete ctx->split_pass[k];
@@ -871,9 +895,7 @@ void lzma_ctx_destroy(lzma_ctx* ctx) {
     }
     if (ctx->rc_stream) hipStreamDestroy(ctx->rc_stream);
     if (ctx->walk_stream) hipStreamDestroy(ctx->walk_stream);
-    ctx->split_recs.release();
-    ctx->split_coder.release();
-    ctx->pin_rc.release();
+
     if (ctx->dec_host) hipHostFree(ctx->dec_host);
     if (ctx->arena) hipFree(ctx->arena);
     if (ctx->litbuf) hipFree(ctx->litbuf);

@@ -349,15 +349,18 @@ class Context:
             if rc != LZMA_E_PARAM:   # a refusal consumes nothing; a failed parse drops every staged batch
                 self._staged = []
             self.check(rc)
-        self._coder_n = staged[0] if staged else 0
+        self._coders = getattr(self, "_coders", []) + [staged[0] if staged else 0]
         self._staged = staged[1:]
 
     def encode_parse_dev_wait(self) -> np.ndarray:
-        """Wait for the range coder; the encoded lengths."""
-        n = getattr(self, "_coder_n", 0)
+        """Wait for the oldest range coder in flight; its batch's encoded lengths."""
+        coders = getattr(self, "_coders", [])
+        n = coders[0] if coders else 0
         lens = np.zeros(max(n, 1), dtype=np.uint64)
-        self.check(lib().lzma_enc_parse_dev_wait(self.h, lens.ctypes.data))
-        self._coder_n = 0
+        rc = lib().lzma_enc_parse_dev_wait(self.h, lens.ctypes.data)
+        if rc != LZMA_E_PARAM:   # collected (or failed): the oldest coder is gone
+            self._coders = coders[1:]
+        self.check(rc)
         return lens[:n]
 
     def pack_dev(self, d_src, src_offs: np.ndarray, lens: np.ndarray, d_dst, stream_ptr: int = 0) -> np.ndarray:

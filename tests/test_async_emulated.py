@@ -118,12 +118,26 @@ def _split_worker(q):
                                                               outs[1].ctypes.data))
         ctx.encode_parse_dev_async()
         ctx.encode_stage_dev(src.ctypes.data, offs, p, outs[1].ctypes.data, caps)
-        r["parse_while_coder_pending"] = refused(lambda: ctx.encode_parse_dev_async())
         lens_a = ctx.encode_parse_dev_wait()
         ctx.encode_parse_dev_async()
         lens_b = ctx.encode_parse_dev_wait()
         r["a_equal"] = got(outs[0], lens_a) == ref
         r["b_equal"] = got(outs[1], lens_b) == ref
+        # two coders in flight (one per slot): B parsed before A's coder is collected; a
+        # third parse is refused until the oldest is collected; the waits return A, then B
+        for o in outs:
+            o[:] = 0
+        ctx.encode_stage_dev(src.ctypes.data, offs, p, outs[0].ctypes.data, caps)
+        ctx.encode_stage_dev(src.ctypes.data, offs, p, outs[1].ctypes.data, caps)
+        ctx.encode_parse_dev_async()
+        ctx.encode_parse_dev_async()
+        ctx.encode_stage_dev(src.ctypes.data, offs, p, outs[2].ctypes.data, caps)
+        r["parse_with_two_coders_pending"] = refused(lambda: ctx.encode_parse_dev_async())
+        lens_a = ctx.encode_parse_dev_wait()
+        ctx.encode_parse_dev_async()
+        lens_b = ctx.encode_parse_dev_wait()
+        lens_c = ctx.encode_parse_dev_wait()
+        r["two_coders_equal"] = got(outs[0], lens_a) == ref and got(outs[1], lens_b) == ref and got(outs[2], lens_c) == ref
         # the round-5 order (bench.py): the next batch staged before the parse, so its walk
         # runs beside it: stage A, stage B, parse A (B's walk), wait A, stage C, parse B
         # (C's walk), wait B, parse C, wait C; a third staged batch is refused

@@ -19,14 +19,17 @@ SIMT = os.path.join(REPO, "tests", "simt")
 
 
 @pytest.mark.timeout(900)
-def test_bench_gpus2_launcher_emulated(tmp_path):
+@pytest.mark.parametrize("steps,warmup", [(1, 0), (4, 2)])
+def test_bench_gpus2_launcher_emulated(tmp_path, steps, warmup):
+    """steps 4 / warmup 2: the lagged split schedule (no parse fence at these stream counts:
+    two batches staged, two range coders in flight) over several steps, verified."""
     subprocess.check_call(["make", "-s", "-j", "8", "-C", SIMT, "so"])
     cont = str(tmp_path / "gathered.lzmg")
     size, chunk = 40000, 5000
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR",
                                                              "MASTER_PORT")}
     out = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--emulate",
-                          "--size", str(size), "--chunk", str(chunk), "--steps", "1", "--warmup", "0",
+                          "--size", str(size), "--chunk", str(chunk), "--steps", str(steps), "--warmup", str(warmup),
                           "--cpu-sample", "0", "--single-stream", "0", "--dump-container", cont],
                          env=env, capture_output=True, text=True, timeout=800)
     assert out.returncode == 0, out.stderr[-3000:]
