@@ -106,13 +106,16 @@ int lzma_pack_dev(lzma_ctx *ctx, const uint8_t *d_src, const uint64_t *h_src_off
  *     on the coder stream; then, if a second batch is staged, waits for its chain count
  *     and enqueues its walk on the walk stream (beside this parser); returns without
  *     waiting for the parser, the coder or that walk.
- *   lzma_enc_parse_dev_wait: waits for the coder; h_out_lens as lzma_enc_batch_dev.
+ *   lzma_enc_parse_dev_wait: waits for the oldest coder in flight; h_out_lens as
+ *     lzma_enc_batch_dev for that batch.
  * One pass per batch: at most 16384 streams and lzma_ctx_set_batch_bytes of input
- * (LZMA_E_PARAM otherwise). Order: stage (once or twice), parse_async, wait, and so on,
- * a stage of the next batch allowed anywhere while at most one other batch is staged
- * (pipelined: stage k + 1, parse_async k, wait k); a second parse_async before wait, or
- * a third staged batch, returns LZMA_E_PARAM, and a failed parse_async drops every
- * staged batch. While a batch is staged or its coder is in flight, the context's other
+ * (LZMA_E_PARAM otherwise). At most two batches staged and two coders in flight (each
+ * staged batch and each coder holds one of the context's two live slots); a third
+ * stage or a parse_async with two coders in flight returns LZMA_E_PARAM, and a failed
+ * parse_async drops every staged batch. Pipelined orders: stage k + 1, parse_async k,
+ * wait k (with a parse fence); or stage 0, stage 1, parse_async 0, stage 2, then per k:
+ * parse_async k + 1, stage k + 3, wait k (without one: parser k + 1 is enqueued while
+ * coder k may still run, and batch k + 2's walk runs beside parser k + 1). While a batch is staged or its coder is in flight, the context's other
  * encode, decode and pack entry points return LZMA_E_PARAM. Reference: Encoder.Code
  * (Encoder.java:1064-1077), as for lzma_enc_batch_dev; the bytes are the same. */
 int lzma_enc_stage_dev(lzma_ctx *ctx, const lzma_params *p,
