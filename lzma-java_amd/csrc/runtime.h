@@ -170,13 +170,14 @@ struct Ctx {
     int split_state = 0;
     // range coders in flight (at most two, one per slot, oldest first): rc_pending = how many
     int rc_pending = 0;
-    int rc_slot[2] = {0, 0}, rc_ns[2] = {0, 0};
+    int rc_slot[2] = {0, 0}, rc_ns[2] = {0, 0};   // rc_slot: the coder set (coder_bind)
     hipEvent_t rc_done[2] = {nullptr, nullptr}, parse_done[2] = {nullptr, nullptr};
     hipEvent_t cnt_done[2] = {nullptr, nullptr};    // per slot: the chain count copied to the host
     hipEvent_t walk_done[2] = {nullptr, nullptr};   // per slot: the walk's verdict copied to the host
+    hipEvent_t parse_start = nullptr;      // the split form: st has reached the parser (past the fence)
     hipStream_t rc_stream = nullptr;       // created on first use
     hipStream_t walk_stream = nullptr;     // a staged pass's walk beside the older pass's parse
-    DevBuf split_recs[2], split_coder[2];  // per slot: the coder's records and per-stream arrays (apart from the arena)
+    DevBuf split_recs[2], split_coder[2];  // per coder set: the coder records and per-stream arrays (apart from the arena)
     HostBuf pin_rc[2];                     // per slot: the coder's lengths and verdicts, written by the device
     // timing
     bool timing = false;

@@ -255,26 +255,15 @@ static int pass_carve(Ctx* ctx, EncPass& P) {
     need_live(cl, P);
     need_shared(cs, P);
     P.carved_arena = ctx->arena;
-    if (P.split) {
-        // records apart from the match finder's buffers; the coder's per-stream arrays apart
-        // from the pass arrays the next pass's staging rewrites
-        const size_t coder_bytes = (size_t)(ns + 1) * 8 * 4 + (size_t)ns * 8 + (size_t)ns * kRcSegs * kRcSegWords * 4 + 4096;
-        DevBuf &R = ctx->split_recs[P.slot], &C = ctx->split_coder[P.slot];
-        if (rec_bytes_all > R.n || coder_bytes > C.n)   // a reallocation waits for the coders in flight
-            for (int q = 0; q < ctx->rc_pending; q++) HIPCHK(hipEventSynchronize(ctx->rc_done[ctx->rc_slot[q]]));
-        if (!R.ensure(std::max<size_t>(rec_bytes_all, 256)) || !C.ensure(coder_bytes))
-            return ctx->fail(LZMA_E_NOMEM, "coder records %zu bytes", rec_bytes_all);
-        P.d_recs = R.as<uint16_t>();
-    }
-    return LZMA_OK;
+    return LZMA_OK;   // the split form binds its coder records when its parse is enqueued (coder_bind)
 }
 
-// The split form: a pass's pointers into the context's shared allocations (the arena's
-// match-finder and parser scratch, the coder records) as of now. Another pass's staging
+// The split form: a pass's pointers into the context's shared arena (the match finder's
+// scratch) as of now. Another pass's staging
 // may have grown, and so moved, them since this pass was carved (it waited for every user
 // of the old ones first); the live buffers are the pass's own slot's and do not move.
 static int pass_refresh_shared(Ctx* ctx, EncPass& P) {
-    if (P.carved_arena == ctx->arena && P.d_recs == ctx->split_recs[P.slot].as<uint16_t>()) return LZMA_OK;
+    if (P.carved_arena == ctx->arena) return LZMA_OK;
     return pass_carve(ctx, P);   // sizes unchanged: no reallocation, the live slot's layout is the same
 }
 
@@ -370,6 +359,11 @@ static int pass_parse(Ctx* ctx, EncPass& P, hipStream_t st) {
         std::lock_guard<std::mutex> g(g_ctx_lock);
         const Ctx* f = ctx->fence;
         if (f && g_live_ctx.count(const_cast<Ctx*>(f)) && f->dec_pending) HIPCHK(hipStreamWaitEvent(st, f->dec_done, 0));
+    }
+    if (P.split) {   // a staged pass's walk waits for this point (runtime.hip enc_parse_dev_async)
+        if (!ctx->parse_start && hipEventCreateWithFlags(&ctx->parse_start, hipEventDisableTiming) != hipSuccess)
+            return ctx->fail(LZMA_E_DEVICE, "parse event");
+        HIPCHK(hipEventRecord(ctx->parse_start, st));
     }
     int rc = launch_encoder(ctx, a, P.wide, P.grid, st);
     if (rc) return rc;
@@ -510,6 +504,23 @@ __global__ void coder_arrays_kernel(int ns, const uint64_t* rofs, const uint64_t
 // Batch k + 1's keys and sorts (which need LDS) then run on st before batch k's parser, and
 // its walk (no LDS, latency-bound) runs on the walk stream beside that parser; batch k + 2's
 // staging waits for it, as its match finder reuses the same scratch.
+// The split form's coder buffers (records, the coder's per-stream arrays, the pinned
+// lengths and verdicts): two sets, one per coder in flight. A pass takes set 0 unless the
+// coder in flight holds it; so a caller that collects each coder before the next parse
+// allocates one set. Returns the set.
+static int coder_bind(Ctx* ctx, EncPass& P, int* set) {
+    const int rb = (ctx->rc_pending == 1 && ctx->rc_slot[0] == 0) ? 1 : 0;   // no coder in flight holds rb
+    const int ns = P.ns;
+    const size_t rec_bytes_all = P.rofs[ns] * 2;
+    const size_t coder_bytes = (size_t)(ns + 1) * 8 * 4 + (size_t)ns * 8 + (size_t)ns * kRcSegs * kRcSegWords * 4 + 4096;
+    if (!ctx->split_recs[rb].ensure(std::max<size_t>(rec_bytes_all, 256)) || !ctx->split_coder[rb].ensure(coder_bytes) ||
+        !ctx->pin_rc[rb].ensure((size_t)ns * 12 + 16))
+        return ctx->fail(LZMA_E_NOMEM, "coder records %zu bytes", rec_bytes_all);
+    P.d_recs = ctx->split_recs[rb].as<uint16_t>();
+    *set = rb;
+    return LZMA_OK;
+}
+
 // the coder's per-stream lengths and verdicts into pinned host memory, on the coder stream
 // behind the coder (a kernel, not a copy: a device-to-host copy queued behind the coder
 // would hold a copy engine that other streams' copies need)
@@ -596,11 +607,11 @@ static int enc_parse_dev_async(Ctx* ctx, hipStream_t st) {
         Q->walk_state = 0;
     }
     if (exp_env("LZG_PROBE_WALK_ONLY")) return LZMA_OK;   // experiment build: concurrency probe (tools/overlap_probe.py)
-    // a coder still in flight on P's slot (its records, its coder arrays): P's parser and the
-    // copy of P's coder arrays wait for it on the device
-    for (int q = 0; q < ctx->rc_pending; q++)
-        if (ctx->rc_slot[q] == P.slot) HIPCHK(hipStreamWaitEvent(st, ctx->rc_done[P.slot], 0));
-    if ((rc = pass_refresh_shared(ctx, P)) || (rc = pass_parse(ctx, P, st))) { ctx->split_state = 0; return rc; }
+    int ps;   // the coder set
+    if ((rc = pass_refresh_shared(ctx, P)) || (rc = coder_bind(ctx, P, &ps)) || (rc = pass_parse(ctx, P, st))) {
+        ctx->split_state = 0;
+        return rc;
+    }
     if (!ctx->rc_stream && hipStreamCreateWithFlags(&ctx->rc_stream, hipStreamNonBlocking) != hipSuccess)
         return ctx->fail(LZMA_E_DEVICE, "coder stream");
     // The newer staged pass's walk beside this parse, on the walk stream: launched after the
@@ -611,12 +622,14 @@ static int enc_parse_dev_async(Ctx* ctx, hipStream_t st) {
     if (Q && Q->walk_state == 0) {
         if (!ctx->walk_stream && hipStreamCreateWithFlags(&ctx->walk_stream, hipStreamNonBlocking) != hipSuccess)
             return ctx->fail(LZMA_E_DEVICE, "walk stream");
+        // not before this parse starts (with a fence it waits for the previous decode): the
+        // walk then runs beside this parse, and does not take the CUs the parse is waiting for
+        HIPCHK(hipStreamWaitEvent(ctx->walk_stream, ctx->parse_start, 0));
         if ((rc = mf_walk_launch(ctx, Q->d, Q->inpad, Q->d_offs, Q->ns, Q->total, Q->wide, Q->w, ctx->walk_stream, Q->slot)))
             return rc;
         HIPCHK(hipEventRecord(ctx->walk_done[Q->slot], ctx->walk_stream));
         Q->walk_state = 1;
     }
-    const int ps = P.slot;
     if (!ctx->parse_done[ps] && hipEventCreateWithFlags(&ctx->parse_done[ps], hipEventDisableTiming) != hipSuccess)
         return ctx->fail(LZMA_E_DEVICE, "parse event");
     if (!ctx->rc_done[ps] && hipEventCreateWithFlags(&ctx->rc_done[ps], hipEventDisableTiming) != hipSuccess)
@@ -632,10 +645,6 @@ static int enc_parse_dev_async(Ctx* ctx, hipStream_t st) {
     HIPCHK(hipEventRecord(ctx->parse_done[ps], st));
     HIPCHK(hipStreamWaitEvent(ctx->rc_stream, ctx->parse_done[ps], 0));
     if ((rc = pass_rc(ctx, P, ca.rofs, ca.rlens, ca.order, ca.status, ca.oofs, ca.lens, ca.seg, ctx->rc_stream))) return rc;
-    if ((size_t)P.ns * 12 + 16 > ctx->pin_rc[ps].n)   // a reallocation waits for a coder still writing there
-        for (int q = 0; q < ctx->rc_pending; q++)
-            if (ctx->rc_slot[q] == ps) HIPCHK(hipEventSynchronize(ctx->rc_done[ps]));
-    if (!ctx->pin_rc[ps].ensure((size_t)P.ns * 12 + 16)) return ctx->fail(LZMA_E_NOMEM, "pinned staging");
     uint64_t* h_lens = ctx->pin_rc[ps].as<uint64_t>();
     hipLaunchKernelGGL(coder_out_kernel, dim3((P.ns + 255) / 256), dim3(256), 0, ctx->rc_stream, P.ns, ca.lens, ca.status,
                        h_lens, (int32_t*)(h_lens + P.ns));
@@ -895,6 +904,7 @@ void lzma_ctx_destroy(lzma_ctx* ctx) {
     }
     if (ctx->rc_stream) hipStreamDestroy(ctx->rc_stream);
     if (ctx->walk_stream) hipStreamDestroy(ctx->walk_stream);
+    if (ctx->parse_start) hipEventDestroy(ctx->parse_start);
 
     if (ctx->dec_host) hipHostFree(ctx->dec_host);
     if (ctx->arena) hipFree(ctx->arena);
