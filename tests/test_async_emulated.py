@@ -167,6 +167,30 @@ def _split_worker(q):
             x, o, c, out, ss = b
             r["next_staged_%d_equal" % k] = [out[int(c[i]):int(c[i]) + int(ln[i])].tobytes() for i in range(len(ss))] == \
                 ctx.encode_batch(ss, p)
+        # the overflow retry of a staged batch whose match-finder scratch the next staged batch
+        # had already refilled (runtime.hip enc_parse_dev_async: `redone`): a fresh context
+        # (no overflow-rate hint), an alphabet of 4 at fb 273 overflows the first pool
+        fresh = lzma_amd.Context(0)
+        p273 = lzma_amd.make_params(dict_size=1 << 20, fb=273, mf=1)
+        ov = np.random.default_rng(4).integers(0, 4, 24000, dtype=np.uint8).tobytes()
+        ob = [batch(len(data), 3000)[:4], None]
+        xo = np.frombuffer(ov + b"\0" * 16, dtype=np.uint8).copy()
+        oo = np.array([0, 15000, 24000], dtype=np.uint64)
+        oc = np.zeros(3, dtype=np.uint64)
+        oc[1:] = np.cumsum([lzma_amd.enc_bound(15000), lzma_amd.enc_bound(9000)])
+        oout = np.zeros(int(oc[-1]) + 1, dtype=np.uint8)
+        x1, o1, c1, out1 = ob[0]
+        fresh.encode_stage_dev(xo.ctypes.data, oo, p273, oout.ctypes.data, oc)
+        fresh.encode_stage_dev(x1.ctypes.data, o1, p273, out1.ctypes.data, c1)
+        fresh.encode_parse_dev_async()   # the first batch's walk overflows: it runs again
+        fresh.encode_parse_dev_async()   # the second batch (staged again after that)
+        la = fresh.encode_parse_dev_wait()
+        lb = fresh.encode_parse_dev_wait()
+        ref_o = fresh.encode_batch([ov[:15000], ov[15000:]], p273)
+        ref_b = fresh.encode_batch([data[int(o1[i]):int(o1[i + 1])] for i in range(len(o1) - 1)], p273)
+        r["retry_first_equal"] = [oout[int(oc[i]):int(oc[i]) + int(la[i])].tobytes() for i in range(2)] == ref_o
+        r["retry_second_equal"] = [out1[int(c1[i]):int(c1[i]) + int(lb[i])].tobytes() for i in range(len(o1) - 1)] == ref_b
+        fresh.close()
         # the synchronous entry points work again once the coder is collected
         r["sync_after"] = ctx.encode_batch(streams[:2], p) == ref[:2]
         # one pass only: a batch above batch_bytes is refused

@@ -479,6 +479,41 @@ def test_gpu_match_lists_equal_oracle(ctx, name, kw, gen):
         assert (counts > 4).mean() > 1 / 8   # the case really overflows the first pool
 
 
+def test_gpu_split_overflow_retry_with_next_staged():
+    """The split encode's overflow retry while a second batch is staged: the first batch's
+    walk overflows the first pool (an alphabet of 4 at fb 273, a fresh context), its match
+    finder runs again over the scratch the second batch's staging had filled, and the
+    second batch is staged again (runtime.hip enc_parse_dev_async, `redone`). Both
+    batches byte-equal to the oracle's Encoder.Code."""
+    torch = pytest.importorskip("torch")
+    data = np.random.default_rng(4).integers(0, 4, 150000, dtype=np.uint8)
+    other = lzma_amd.bench_generate(1 << 20)
+    p = lzma_amd.make_params(dict_size=1 << 20, fb=273, mf=1)
+    st = torch.cuda.current_stream().cuda_stream
+    fresh = lzma_amd.Context(0)   # no overflow-rate hint from earlier calls
+    try:
+        outs = []
+        for x, cuts in ((data, [0, 90000, 150000]), (other, [0, 300000, 700000, 1 << 20])):
+            offs = np.array(cuts, dtype=np.uint64)
+            oo = np.zeros(len(cuts), dtype=np.uint64)
+            oo[1:] = np.cumsum([lzma_amd.enc_bound(cuts[i + 1] - cuts[i]) for i in range(len(cuts) - 1)])
+            d_in, d_out = torch.from_numpy(x).cuda(), torch.empty(int(oo[-1]), dtype=torch.uint8, device="cuda")
+            fresh.encode_stage_dev(d_in, offs, p, d_out, oo, st)
+            outs.append((x, offs, oo, d_in, d_out))
+        fresh.encode_parse_dev_async(st)
+        fresh.encode_parse_dev_async(st)
+        lens = [fresh.encode_parse_dev_wait(), fresh.encode_parse_dev_wait()]
+        torch.cuda.synchronize()
+        for (x, offs, oo, _, d_out), ln in zip(outs, lens):
+            h = d_out.cpu().numpy()
+            n = len(offs) - 1
+            refs = orc.encode_many([x[int(offs[i]):int(offs[i + 1])].tobytes() for i in range(n)], _oparams(p))
+            for i in range(n):
+                assert h[int(oo[i]):int(oo[i] + ln[i])].tobytes() == refs[i], (n, i)
+    finally:
+        fresh.close()
+
+
 def test_gpu_overflow_retry_encode_equals_oracle(ctx):
     """The encoder consumes the regrown overflow pool: bytes equal Encoder.Code."""
     data = np.random.default_rng(4).integers(0, 4, 150000, dtype=np.uint8).tobytes()
