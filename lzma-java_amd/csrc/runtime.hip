@@ -500,10 +500,12 @@ __global__ void coder_arrays_kernel(int ns, const uint64_t* rofs, const uint64_t
 }
 
 // The split form holds up to two staged passes (slots 0 / 1 of the live buffers, pinned
-// words and events). Steady state, as bench.py calls it: stage(k + 1), then parse_async(k).
-// Batch k + 1's keys and sorts (which need LDS) then run on st before batch k's parser, and
-// its walk (no LDS, latency-bound) runs on the walk stream beside that parser; batch k + 2's
-// staging waits for it, as its match finder reuses the same scratch.
+// words and events) and up to two range coders in flight (coder_bind). Without a parse
+// fence bench.py keeps two batches staged: batch k + 1's keys and sorts (which need LDS)
+// run on st before batch k's parser, its walk (no LDS, latency-bound) on the walk stream
+// beside that parser, and batch k + 2's staging waits for that walk, as its match finder
+// reuses the same scratch. With a fence it stages one batch at a time (stage k + 1 after
+// parse_async k).
 // The split form's coder buffers (records, the coder's per-stream arrays, the pinned
 // lengths and verdicts): two sets, one per coder in flight. A pass takes set 0 unless the
 // coder in flight holds it; so a caller that collects each coder before the next parse
