@@ -388,20 +388,38 @@ def run_pass(args, D, p, ctxs, strong, rank, world, dist):
                     f.write(blob)
     # one buffer encoded, packed and decoded back to back (no pipelining): what a single
     # step costs on its own, reported beside the pipelined steady-state value
+    # Its kernels are timed with HIP events and the library's host-side stalls (buffer
+    # reallocations, whole-device syncs) counted, so the line shows where its time goes
+    for c in (ctx, ctx_dec):
+        c.set_timing(True)
+        c.reset_timings()
+    stats0 = [c.stats() for c in (ctx, ctx_dec)]
     barrier()
     t1 = time.perf_counter()
     lens1 = ctx.encode_batch_dev(d_in, offs, p, d_comp, cap_offs, st)
+    t_e = time.perf_counter()
     pk1 = ctx.pack_dev(d_comp, cap_offs, lens1, d_packs[0], st)
+    t_p = time.perf_counter()
     dl1, ds1 = ctx_dec.decode_batch_dev(props, d_packs[0], pk1, out_sizes, d_dec, offs, st_dec)
     barrier()
     seq_elapsed = time.perf_counter() - t1
+    seq_wall = {"encode_ms": (t_e - t1) * 1e3, "pack_ms": (t_p - t_e) * 1e3, "decode_ms": (t1 + seq_elapsed - t_p) * 1e3}
+    seq_kernels = ctx.timings()
+    seq_kernels.update(ctx_dec.timings())
+    seq_stats = {}
+    for name, c, s0 in (("encoder", ctx, stats0[0]), ("decoder", ctx_dec, stats0[1])):
+        s1 = c.stats()
+        seq_stats[name] = {k: s1[k] - s0[k] for k in s1}
+    for c in (ctx, ctx_dec):
+        c.set_timing(False)
     seq_ok = bool((ds1 == 0).all()) and bool((dl1 == out_sizes).all()) and bool(np.array_equal(lens1, state["lens"]))
     if dist:
         t = torch.tensor([seq_elapsed], dtype=torch.float64, device=D.dev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         seq_elapsed = float(t.item())
     return {"elapsed": elapsed, "timings": timings, "state": state, "host": host, "full": full, "offs": offs,
-            "seq_elapsed": seq_elapsed, "seq_ok": seq_ok, "fence": fence,
+            "seq_elapsed": seq_elapsed, "seq_ok": seq_ok, "fence": fence, "seq_wall": seq_wall,
+            "seq_kernels": seq_kernels, "seq_stats": seq_stats,
             "n": n, "n_all": n_all, "size": size, "my_size": my_size, "comp_bytes": comp_bytes,
             "roundtrip": roundtrip, "t_enc": state["t_enc"], "t_dec": state["t_dec"], "gathered": gathered,
             "bufs": (d_in, d_comp, d_packs, d_dec)}
@@ -545,9 +563,13 @@ def main():
                              args.pipeline, "range coder (the encoder's coder stream), pack and "
                              if args.pipeline == "split" else "")),
             "sequential": {"value": size / r["seq_elapsed"] / 1e6, "unit": "MB/s", "ms": r["seq_elapsed"] * 1e3,
-                           "lengths_equal_timed_steps": r["seq_ok"],
+                           "lengths_equal_timed_steps": r["seq_ok"], "wall_ms": r["seq_wall"],
+                           "kernels_ms": {k: {"total_ms": v[0], "launches": v[1]} for k, v in r["seq_kernels"].items()},
+                           "library_stalls": r["seq_stats"],
                            "note": "one buffer encoded, packed and decoded back to back after the timed loop (no "
-                                   "pipelining): the cost of one step on its own; value is the pipelined steady state"},
+                                   "pipelining): the cost of one step on its own; value is the pipelined steady state. "
+                                   "kernels_ms: HIP events on the launch streams; library_stalls: the library's "
+                                   "buffer reallocations and whole-device syncs during the leg (lzma_ctx_stats)"},
             "parse_fence": r["fence"],
             "ratio": ratio, "chunking": chunking, "verified": ok,
             "verified_means": "every stream decodes to its input and every sampled stream's bytes equal the "

@@ -74,6 +74,15 @@ int lzma_ctx_set_timing(lzma_ctx *ctx, int on);
 /* names[i] / ms[i] / launches[i] for up to cap kernels; returns count. */
 int lzma_ctx_timings(lzma_ctx *ctx, const char **names, double *ms, int64_t *launches, int cap);
 void lzma_ctx_reset_timings(lzma_ctx *ctx);
+/* Host-side stalls of the context so far (cumulative; any pointer may be NULL):
+ * allocations of its own device / pinned buffers (each one a hipFree + hipMalloc of a grown
+ * buffer, hipMalloc of >100 GB workspaces costing tens of ms) with their bytes, and
+ * whole-device synchronisations (hipDeviceSynchronize: a reallocation while a split encode is
+ * in flight, an overflow-pool retry). A caller that reuses one batch layout must see none of
+ * them after its first call: bench.py reports them for its sequential leg, and
+ * tests/test_async_emulated.py asserts none after odd and even counts of split passes.
+ * No reference counterpart (the Java encoder allocates per Create, Encoder.java:224-245). */
+int lzma_ctx_stats(const lzma_ctx *ctx, uint64_t *allocations, uint64_t *alloc_bytes, uint64_t *device_syncs);
 
 /* ---- encode -------------------------------------------------------------
  * Device-resident batch: stream i is d_in[h_offs[i] .. h_offs[i+1]).
@@ -111,8 +120,12 @@ int lzma_pack_dev(lzma_ctx *ctx, const uint8_t *d_src, const uint64_t *h_src_off
  * One pass per batch: at most 16384 streams and lzma_ctx_set_batch_bytes of input
  * (LZMA_E_PARAM otherwise). At most two batches staged and two coders in flight (each
  * staged batch and each coder holds one of the context's two live slots); a third
- * stage or a parse_async with two coders in flight returns LZMA_E_PARAM, and a failed
- * parse_async drops every staged batch. Pipelined orders: stage k + 1, parse_async k,
+ * stage or a parse_async with two coders in flight returns LZMA_E_PARAM, and consumes
+ * nothing; any other failure of parse_async (never LZMA_E_PARAM once the oldest batch is
+ * consumed) drops every staged batch. Without a parse fence, the round-4 order (stage A,
+ * parse_async A, stage B, wait A) blocks the host in stage B until parser A has finished
+ * (B is staged alone, so its walk is enqueued there, sized by a host read of its chain
+ * count behind parser A on hip_stream): stage B before parse_async A to keep the overlap. Pipelined orders: stage k + 1, parse_async k,
  * wait k (with a parse fence); or stage 0, stage 1, parse_async 0, stage 2, then per k:
  * parse_async k + 1, stage k + 3, wait k (without one: parser k + 1 is enqueued while
  * coder k may still run, and batch k + 2's walk runs beside parser k + 1). While a batch is staged or its coder is in flight, the context's other

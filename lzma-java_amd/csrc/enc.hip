@@ -1773,7 +1773,8 @@ int launch_encoder(Ctx* ctx, const EncArgs& a0, bool wide_pairs, int grid, hipSt
     if (a0.pair_bytes != (wide_pairs ? 8u : 4u)) return ctx->fail(LZMA_E_INTERNAL, "pair width mismatch");
     EncArgs a = a0;
     size_t lds = enc_lds_bytes(a);
-    if (lds > 160 * 1024) return ctx->fail(LZMA_E_PARAM, "encoder LDS %zu too large", lds);
+    // + the 16-byte static placeholder every kernel but SPEC 1 declares beside its dynamic LDS
+    if (lds + 16 > 160 * 1024) return ctx->fail(LZMA_E_PARAM, "encoder LDS %zu too large", lds);
 #ifdef LZG_ONLY_SPEC1_LIT   // code-inspection builds (assembly of one kernel family)
     if (!wide_pairs) {
         if (a.lit_in_lds) launch_spec<uint32_t, true, 2, 1>(ctx, a, grid, lds, st);

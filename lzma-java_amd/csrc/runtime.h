@@ -88,11 +88,14 @@ constexpr uint32_t kMctxMagic = 0x584D5A4Cu;   // "LZMX" (multi.hip)
 struct DevBuf {
     void* p = nullptr;
     size_t n = 0;
+    uint64_t allocs = 0, alloc_bytes = 0;   // reallocations (lzma_ctx_stats)
     bool ensure(size_t want) {
         if (want <= n) return true;
         if (p) hipFree(p);
         p = nullptr;
         n = 0;
+        allocs++;
+        alloc_bytes += want;
         if (hipMalloc(&p, want) != hipSuccess) return false;
         n = want;
         return true;
@@ -111,11 +114,14 @@ struct DevBuf {
 struct HostBuf {
     void* p = nullptr;
     size_t n = 0;
+    uint64_t allocs = 0, alloc_bytes = 0;   // reallocations (lzma_ctx_stats)
     bool ensure(size_t want) {
         if (want <= n) return true;
         if (p) hipHostFree(p);
         p = nullptr;
         n = 0;
+        allocs++;
+        alloc_bytes += want;
         if (hipHostMalloc(&p, want, 0) != hipSuccess) return false;
         n = want;
         return true;
@@ -187,6 +193,19 @@ struct Ctx {
     struct Acc { double ms = 0; int64_t n = 0; };
     std::map<std::string, Acc> acc;
 
+    // Host-side events that stall a pipelined caller (lzma_ctx_stats): allocations of the
+    // context's own buffers (hipMalloc / hipHostMalloc after a hipFree of the smaller one) and
+    // whole-device synchronisations. The DevBuf / HostBuf members count their own.
+    uint64_t stat_allocs = 0, stat_alloc_bytes = 0, stat_device_syncs = 0;
+    hipError_t device_sync() {
+        stat_device_syncs++;
+        return hipDeviceSynchronize();
+    }
+    void count_alloc(size_t n) {
+        stat_allocs++;
+        stat_alloc_bytes += n;
+    }
+
     int fail(int code, const char* fmt, ...) {
         char buf[512];
         va_list ap;
@@ -202,6 +221,7 @@ struct Ctx {
             if (tmp) hipFree(tmp);
             tmp = nullptr;
             tmp_size = 0;
+            count_alloc(n);
             if (hipMalloc(&tmp, n) != hipSuccess) return nullptr;
             tmp_size = n;
         }
@@ -217,6 +237,7 @@ struct Ctx {
         if (litbuf) hipFree(litbuf);
         litbuf = nullptr;
         litbuf_size = 0;
+        count_alloc(n);
         if (hipMalloc(&litbuf, n) != hipSuccess) return false;
         litbuf_size = n;
         return true;
@@ -226,6 +247,7 @@ struct Ctx {
         if (arena) hipFree(arena);
         arena = nullptr;
         arena_size = 0;
+        count_alloc(n);
         if (hipMalloc(&arena, n) != hipSuccess) return false;
         arena_size = n;
         return true;

@@ -246,7 +246,7 @@ static int pass_carve(Ctx* ctx, EncPass& P) {
         if (pl.off + 4096 > L.n || ps.off + 4096 > ctx->arena_size) {
             // a reallocation waits for everything that may still read the old buffers: the
             // other staged pass's walk, the older pass's parse, the coder's caller
-            if (ctx->split_state || ctx->rc_pending) HIPCHK(hipDeviceSynchronize());
+            if (ctx->split_state || ctx->rc_pending) HIPCHK(ctx->device_sync());
             if (!L.ensure(pl.off + 4096)) return ctx->fail(LZMA_E_NOMEM, "device workspace %zu bytes", pl.off);
             if (!ctx->ensure_arena(ps.off + 4096)) return ctx->fail(LZMA_E_NOMEM, "device workspace %zu bytes", ps.off);
         }
@@ -320,7 +320,7 @@ static int pass_mf_back(Ctx* ctx, EncPass& P, hipStream_t st, bool* redone = nul
         ctx->ovf_hint = P.slots_per_k;
         P.ovf_cap = P.pool_cap(P.slots_per_k);
         if (redone) *redone = true;
-        HIPCHK(hipDeviceSynchronize());   // rare: the staging below reuses pinned memory other copies may read
+        HIPCHK(ctx->device_sync());   // rare: the staging below reuses pinned memory other copies may read
         if ((rc = pass_carve(ctx, P)) || (rc = pass_stage(ctx, P, st)) ||
             (rc = mf_front(ctx, P.d, P.inpad, P.d_offs, P.ns, P.total, P.wide, P.w, st)))
             return rc;
@@ -329,6 +329,9 @@ static int pass_mf_back(Ctx* ctx, EncPass& P, hipStream_t st, bool* redone = nul
 }
 
 static int pass_parse(Ctx* ctx, EncPass& P, hipStream_t st) {
+    // the walk-subset timing hook leaves the skipped positions' records holding the walk's
+    // inputs (mf_prev2_kernel), not match lists: such a pass is never parsed
+    if (exp_env("LZG_WALK_ONLY")) return ctx->fail(LZMA_E_PARAM, "LZG_WALK_ONLY (a walk timing experiment): no parse");
     EncArgs a{};
     a.in = P.inpad; a.offs = P.d_offs; a.order = P.d_order; a.nstreams = P.ns; a.next = P.d_next;
     a.pairs = P.w.pairs; a.ovf_off = P.w.ovf_off; a.ovf = P.w.ovf;
@@ -398,6 +401,12 @@ static int encode_pass(Ctx* ctx, const Derived& d, const uint8_t* d_in, const ui
         return ctx->fail(LZMA_E_PARAM, "a split encode is in flight on this context: lzma_enc_parse_dev_async / _wait first");
     EncPass P;
     pass_plan(ctx, P, d, d_in, h_offs, s0, s1, d_out, h_out_offs, false);
+    // Nothing is staged, so either live slot is free: take the larger one. A split schedule
+    // that stages one batch at a time (the fenced bench) only ever grows slot 1, and a
+    // synchronous pass fixed to slot 0 then paid a first hipMalloc of ~46 B per input byte
+    // (bench.py's `sequential` leg after the pipelined loop: 1,441.6 ms in the driver's
+    // round-5 record; tests/test_async_emulated.py counts the allocations).
+    P.slot = ctx->live[1].n > ctx->live[0].n ? 1 : 0;
     int rc;
     if ((rc = pass_carve(ctx, P)) || (rc = pass_stage(ctx, P, st)) ||
         (rc = mf_front(ctx, P.d, P.inpad, P.d_offs, P.ns, P.total, P.wide, P.w, st)) || (rc = pass_mf_back(ctx, P, st)))
@@ -592,9 +601,36 @@ static int enc_stage_dev(Ctx* ctx, const lzma_params* p, const uint8_t* d_in, co
     return LZMA_OK;
 }
 
+// Experiment build only: fail the named step of lzma_enc_parse_dev_async (LZG_FAIL_AT =
+// "walk2": the newer staged batch's walk launch; "rc": the coder launch), so the CPU
+// emulation can check that a failure after the oldest batch is consumed drops every staged
+// batch (tests/test_async_emulated.py).
+static bool inject_fail(const char* step) {
+    const char* e = exp_env("LZG_FAIL_AT");
+    return e && strcmp(e, step) == 0;
+}
+
+static int enc_parse_dev_async_body(Ctx* ctx, hipStream_t st);
+
+// A refusal (LZMA_E_PARAM before anything is consumed) leaves the staged batches as they were.
+// Once the oldest staged batch is consumed, any failure drops every staged batch (split_state
+// 0, the newer batch's walk forgotten) and is never reported as LZMA_E_PARAM, so a caller
+// (lzma_amd's wrapper) can tell the two apart by the code alone (include/lzma_mi355x.h).
 static int enc_parse_dev_async(Ctx* ctx, hipStream_t st) {
     if (!ctx->split_state) return ctx->fail(LZMA_E_PARAM, "nothing staged: lzma_enc_stage_dev first");
     if (ctx->rc_pending >= 2) return ctx->fail(LZMA_E_PARAM, "two coders are in flight: lzma_enc_parse_dev_wait first");
+    const int rc = enc_parse_dev_async_body(ctx, st);
+    if (rc == LZMA_OK) return rc;
+    ctx->split_state = 0;
+    for (int k = 0; k < 2; k++)
+        if (ctx->split_pass[k]) ctx->split_pass[k]->walk_state = 0;
+    // what was enqueued before the failure (the newer batch's walk, this batch's parser) may
+    // still run over the buffers the next staging reuses: let it drain (a failure path only)
+    (void)ctx->device_sync();
+    return rc == LZMA_E_PARAM ? LZMA_E_INTERNAL : rc;
+}
+
+static int enc_parse_dev_async_body(Ctx* ctx, hipStream_t st) {
     EncPass& P = *ctx->split_pass[ctx->split_head];
     // from here on the oldest staged pass is consumed (or failed)
     ctx->split_head = (ctx->split_head + 1) % 2;
@@ -602,18 +638,16 @@ static int enc_parse_dev_async(Ctx* ctx, hipStream_t st) {
     EncPass* Q = ctx->split_state ? ctx->split_pass[ctx->split_head] : nullptr;   // the newer staged pass
     int rc;
     bool redone = false;
-    if ((rc = pass_mf_back(ctx, P, st, &redone))) { ctx->split_state = 0; return rc; }
+    if ((rc = pass_mf_back(ctx, P, st, &redone))) return rc;
     if (redone && Q) {   // P's match finder ran again over the scratch Q's staging had filled
         if ((rc = pass_refresh_shared(ctx, *Q)) || (rc = pass_stage(ctx, *Q, st)) || (rc = mf_front(ctx, Q->d, Q->inpad, Q->d_offs, Q->ns, Q->total, Q->wide, Q->w, st)) ||
-            (rc = mf_count_enqueue(ctx, Q->w, Q->ns, st, Q->slot))) { ctx->split_state = 0; return rc; }
+            (rc = mf_count_enqueue(ctx, Q->w, Q->ns, st, Q->slot)))
+            return rc;
         Q->walk_state = 0;
     }
     if (exp_env("LZG_PROBE_WALK_ONLY")) return LZMA_OK;   // experiment build: concurrency probe (tools/overlap_probe.py)
     int ps;   // the coder set
-    if ((rc = pass_refresh_shared(ctx, P)) || (rc = coder_bind(ctx, P, &ps)) || (rc = pass_parse(ctx, P, st))) {
-        ctx->split_state = 0;
-        return rc;
-    }
+    if ((rc = pass_refresh_shared(ctx, P)) || (rc = coder_bind(ctx, P, &ps)) || (rc = pass_parse(ctx, P, st))) return rc;
     if (!ctx->rc_stream && hipStreamCreateWithFlags(&ctx->rc_stream, hipStreamNonBlocking) != hipSuccess)
         return ctx->fail(LZMA_E_DEVICE, "coder stream");
     // The newer staged pass's walk beside this parse, on the walk stream: launched after the
@@ -627,6 +661,7 @@ static int enc_parse_dev_async(Ctx* ctx, hipStream_t st) {
         // not before this parse starts (with a fence it waits for the previous decode): the
         // walk then runs beside this parse, and does not take the CUs the parse is waiting for
         HIPCHK(hipStreamWaitEvent(ctx->walk_stream, ctx->parse_start, 0));
+        if (inject_fail("walk2")) return ctx->fail(LZMA_E_DEVICE, "injected failure (LZG_FAIL_AT=walk2)");
         if ((rc = mf_walk_launch(ctx, Q->d, Q->inpad, Q->d_offs, Q->ns, Q->total, Q->wide, Q->w, ctx->walk_stream, Q->slot)))
             return rc;
         HIPCHK(hipEventRecord(ctx->walk_done[Q->slot], ctx->walk_stream));
@@ -646,6 +681,7 @@ static int enc_parse_dev_async(Ctx* ctx, hipStream_t st) {
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(ctx->parse_done[ps], st));
     HIPCHK(hipStreamWaitEvent(ctx->rc_stream, ctx->parse_done[ps], 0));
+    if (inject_fail("rc")) return ctx->fail(LZMA_E_DEVICE, "injected failure (LZG_FAIL_AT=rc)");
     if ((rc = pass_rc(ctx, P, ca.rofs, ca.rlens, ca.order, ca.status, ca.oofs, ca.lens, ca.seg, ctx->rc_stream))) return rc;
     uint64_t* h_lens = ctx->pin_rc[ps].as<uint64_t>();
     hipLaunchKernelGGL(coder_out_kernel, dim3((P.ns + 255) / 256), dim3(256), 0, ctx->rc_stream, P.ns, ca.lens, ca.status,
@@ -761,6 +797,7 @@ static int decode_batch_dev_async(Ctx* ctx, const uint8_t props[5], const uint8_
         if (ctx->dec_host) hipHostFree(ctx->dec_host);
         ctx->dec_host = nullptr;
         ctx->dec_host_words = 0;
+        ctx->count_alloc(words * 8);
         if (hipHostMalloc((void**)&ctx->dec_host, words * 8, hipHostMallocDefault) != hipSuccess)
             return ctx->fail(LZMA_E_NOMEM, "pinned decode staging");
         ctx->dec_host_words = words;
@@ -945,6 +982,20 @@ int lzma_ctx_timings(lzma_ctx* ctx, const char** names, double* ms, int64_t* lau
         i++;
     }
     return i;
+}
+
+int lzma_ctx_stats(const lzma_ctx* ctx, uint64_t* allocations, uint64_t* alloc_bytes, uint64_t* device_syncs) {
+    if (!ok_ctx(ctx)) return LZMA_E_PARAM;
+    uint64_t n = ctx->stat_allocs, b = ctx->stat_alloc_bytes;
+    auto add = [&](uint64_t k, uint64_t kb) { n += k; b += kb; };
+    for (const DevBuf* d : {&ctx->io_in, &ctx->io_out, &ctx->io_pack, &ctx->io_offs, &ctx->live[0], &ctx->live[1],
+                            &ctx->split_recs[0], &ctx->split_recs[1], &ctx->split_coder[0], &ctx->split_coder[1]})
+        add(d->allocs, d->alloc_bytes);
+    for (const HostBuf* h : {&ctx->pin, &ctx->pin_mf, &ctx->pin_rc[0], &ctx->pin_rc[1]}) add(h->allocs, h->alloc_bytes);
+    if (allocations) *allocations = n;
+    if (alloc_bytes) *alloc_bytes = b;
+    if (device_syncs) *device_syncs = ctx->stat_device_syncs;
+    return LZMA_OK;
 }
 
 void lzma_ctx_reset_timings(lzma_ctx* ctx) {

@@ -38,7 +38,7 @@ LZMA_E_INTERNAL = -7
 EXPORTED_SYMBOLS = [
     "lzma_version", "lzma_params_default", "lzma_params_check", "lzma_write_props", "lzma_read_props",
     "lzma_enc_bound", "lzma_ctx_create", "lzma_ctx_destroy", "lzma_last_error", "lzma_ctx_set_batch_bytes",
-    "lzma_ctx_set_timing", "lzma_ctx_timings", "lzma_ctx_reset_timings", "lzma_enc_batch_dev", "lzma_enc_batch",
+    "lzma_ctx_set_timing", "lzma_ctx_timings", "lzma_ctx_reset_timings", "lzma_ctx_stats", "lzma_enc_batch_dev", "lzma_enc_batch",
     "lzma_pack_dev",
     "lzma_encode", "lzma_dec_batch_dev", "lzma_dec_batch", "lzma_decode", "lzma_bench_generate",
     "lzma_rnd_generate", "lzma_text_generate", "lzma_match_lists",
@@ -100,6 +100,7 @@ def lib():
         L.lzma_ctx_set_timing.argtypes = [vp, i32]
         L.lzma_ctx_timings.argtypes = [vp, vp, vp, vp, i32]
         L.lzma_ctx_reset_timings.argtypes = [vp]
+        L.lzma_ctx_stats.argtypes = [vp, vp, vp, vp]
         L.lzma_enc_batch_dev.argtypes = [vp, P, vp, vp, i32, vp, vp, vp, vp]
         L.lzma_enc_batch.argtypes = [vp, P, vp, vp, i32, vp, u64, vp]
         L.lzma_pack_dev.argtypes = [vp, vp, vp, vp, i32, vp, vp, vp]
@@ -253,6 +254,12 @@ class Context:
 
     def reset_timings(self):
         lib().lzma_ctx_reset_timings(self.h)
+
+    def stats(self) -> dict:
+        """lzma_ctx_stats: cumulative allocations (count, bytes) and whole-device syncs."""
+        v = (ctypes.c_uint64 * 3)()
+        self.check(lib().lzma_ctx_stats(self.h, ctypes.byref(v, 0), ctypes.byref(v, 8), ctypes.byref(v, 16)))
+        return {"allocations": int(v[0]), "alloc_bytes": int(v[1]), "device_syncs": int(v[2])}
 
     # ---- host-buffer batch API
     def encode_batch(self, streams: Sequence[bytes], p: Params) -> List[bytes]:

@@ -217,3 +217,152 @@ def test_split_encode_emulated():
     pr.join(timeout=60)
     assert "error" not in r, r.get("error")
     assert all(r.values()), r
+
+
+def _seq_leg_worker(q, passes, fenced):
+    """bench.py's schedule in miniature: `passes` split passes (fenced: stage k + 1 after
+    parse k, as at 16 streams per CU; unfenced: two batches staged, two coders in flight),
+    then the sequential leg (synchronous encode, pack, decode) on the same buffers."""
+    import lzma_amd
+    lzma_amd.LIB_PATH = SIMT_LIB   # "device" pointers are host pointers in the emulation
+    try:
+        data = lzma_amd.bench_generate(6 * 2000 - 321).tobytes()
+        streams = [data[i:i + 2000] for i in range(0, len(data), 2000)]
+        p = lzma_amd.make_params(dict_size=1 << 20, fb=32)
+        props = lzma_amd.write_props(p)
+        src = np.frombuffer(data + b"\0" * 16, dtype=np.uint8).copy()
+        offs = np.zeros(len(streams) + 1, dtype=np.uint64)
+        offs[1:] = np.cumsum([len(s) for s in streams])
+        caps = np.zeros(len(streams) + 1, dtype=np.uint64)
+        caps[1:] = np.cumsum([lzma_amd.enc_bound(len(s)) for s in streams])
+        comps = [np.zeros(int(caps[-1]) + 1, dtype=np.uint8) for _ in range(2)]
+        pack = np.zeros(int(caps[-1]) + 1, dtype=np.uint8)
+        dec_out = np.zeros(len(data) + 1, dtype=np.uint8)
+        sizes = np.array([len(s) for s in streams], dtype=np.int64)
+        enc, dec = lzma_amd.Context(0), lzma_amd.Context(0)
+        if fenced:
+            enc.set_parse_fence(dec)
+            enc.encode_stage_dev(src.ctypes.data, offs, p, comps[0].ctypes.data, caps)
+            for k in range(passes):
+                enc.encode_parse_dev_async()
+                if k + 1 < passes:
+                    enc.encode_stage_dev(src.ctypes.data, offs, p, comps[0].ctypes.data, caps)
+                lens = enc.encode_parse_dev_wait()
+                pk = dec.pack_dev(comps[0].ctypes.data, caps, lens, pack.ctypes.data)
+                dec.decode_batch_dev_async(props, pack.ctypes.data, pk, sizes, dec_out.ctypes.data, offs)
+                dec.decode_batch_dev_wait()
+            enc.set_parse_fence(None)
+        else:
+            stage = lambda j: enc.encode_stage_dev(src.ctypes.data, offs, p, comps[j % 2].ctypes.data, caps)
+            stage(0)
+            if passes > 1:
+                stage(1)
+            enc.encode_parse_dev_async()
+            if passes > 2:
+                stage(2)
+            for k in range(passes):
+                if k + 1 < passes:
+                    enc.encode_parse_dev_async()
+                    if k + 3 < passes:
+                        stage(k + 3)
+                lens = enc.encode_parse_dev_wait()
+                pk = dec.pack_dev(comps[k % 2].ctypes.data, caps, lens, pack.ctypes.data)
+                dec.decode_batch_dev(props, pack.ctypes.data, pk, sizes, dec_out.ctypes.data, offs)
+        s0 = (enc.stats(), dec.stats())
+        lens1 = enc.encode_batch_dev(src.ctypes.data, offs, p, comps[0].ctypes.data, caps)
+        pk1 = enc.pack_dev(comps[0].ctypes.data, caps, lens1, pack.ctypes.data)
+        dl, ds = dec.decode_batch_dev(props, pack.ctypes.data, pk1, sizes, dec_out.ctypes.data, offs)
+        s1 = (enc.stats(), dec.stats())
+        ok = bool((ds == 0).all()) and dec_out[:len(data)].tobytes() == data and np.array_equal(lens1, lens)
+        enc.close()
+        dec.close()
+        q.put(dict(ok=ok, delta=[{k: b[k] - a[k] for k in a} for a, b in zip(s0, s1)], before=s0))
+    except BaseException as e:   # reported to the parent
+        q.put(dict(error=repr(e)))
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("fenced", [True, False])
+@pytest.mark.parametrize("passes", [4, 5])
+def test_sequential_leg_allocates_nothing_after_split_passes(passes, fenced):
+    """VERDICT r05 (weak 3): bench.py's `sequential` leg (one synchronous encode + pack +
+    decode after the pipelined loop) must not reallocate the context's workspaces or
+    synchronise the whole device, whatever the parity of the split passes before it (the
+    driver ran 25, the builder's runs 4 and 22). lzma_ctx_stats counts both."""
+    subprocess.check_call(["make", "-s", "-j", "8", "-C", SIMT, "so"])
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    pr = ctx.Process(target=_seq_leg_worker, args=(q, passes, fenced))
+    pr.start()
+    r = q.get(timeout=500)
+    pr.join(timeout=60)
+    assert "error" not in r, r.get("error")
+    assert r["ok"]
+    assert r["before"][0]["allocations"] > 0   # the counters count (the split passes allocated)
+    for d in r["delta"]:
+        assert d == {"allocations": 0, "alloc_bytes": 0, "device_syncs": 0}, r
+
+
+SIMT_EXP_LIB = os.path.join(SIMT, "build", "so_exp", "libsimt_lzma.so")
+
+
+def _inject_worker(q, where):
+    os.environ["LZG_FAIL_AT"] = where   # read by the experiment build only
+    import lzma_amd
+    lzma_amd.LIB_PATH = SIMT_EXP_LIB
+    try:
+        data = lzma_amd.bench_generate(4 * 2500 - 99).tobytes()
+        streams = [data[i:i + 2500] for i in range(0, len(data), 2500)]
+        p = lzma_amd.make_params(dict_size=1 << 20, fb=32)
+        src = np.frombuffer(data + b"\0" * 16, dtype=np.uint8).copy()
+        offs = np.zeros(len(streams) + 1, dtype=np.uint64)
+        offs[1:] = np.cumsum([len(s) for s in streams])
+        caps = np.zeros(len(streams) + 1, dtype=np.uint64)
+        caps[1:] = np.cumsum([lzma_amd.enc_bound(len(s)) for s in streams])
+        outs = [np.zeros(int(caps[-1]) + 1, dtype=np.uint8) for _ in range(2)]
+        ctx = lzma_amd.Context(0)
+        r = {}
+        ctx.encode_stage_dev(src.ctypes.data, offs, p, outs[0].ctypes.data, caps)
+        ctx.encode_stage_dev(src.ctypes.data, offs, p, outs[1].ctypes.data, caps)
+        try:
+            ctx.encode_parse_dev_async()
+            r["failed"] = False
+        except lzma_amd.LzmaError as e:
+            r["failed"] = True
+            r["code_not_param"] = e.code != lzma_amd.LZMA_E_PARAM
+        r["wrapper_dropped"] = getattr(ctx, "_staged", []) == []
+        try:   # nothing is staged any more: a refusal
+            ctx.encode_parse_dev_async()
+            r["then_refused"] = False
+        except lzma_amd.LzmaError as e:
+            r["then_refused"] = e.code == lzma_amd.LZMA_E_PARAM
+        os.environ["LZG_FAIL_AT"] = ""
+        # the context works again: stage, parse, wait; the bytes equal the synchronous encode's
+        ref = ctx.encode_batch(streams, p)
+        ctx.encode_stage_dev(src.ctypes.data, offs, p, outs[0].ctypes.data, caps)
+        ctx.encode_parse_dev_async()
+        lens = ctx.encode_parse_dev_wait()
+        r["after_equal"] = [outs[0][int(caps[i]):int(caps[i]) + int(lens[i])].tobytes() for i in range(len(streams))] == ref
+        ctx.close()
+        q.put(r)
+    except BaseException as e:   # reported to the parent
+        q.put(dict(error=repr(e)))
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("where", ["walk2", "rc"])
+def test_split_failure_after_consumption_drops_staged(where):
+    """a failure of lzma_enc_parse_dev_async after the oldest staged batch is
+    consumed (the newer batch's walk launch, the coder launch; injected in the experiment
+    build) drops every staged batch on the C side and in the wrapper alike, is not reported
+    as a refusal, and the context encodes correctly afterwards."""
+    subprocess.check_call(["make", "-s", "-j", "8", "-C", SIMT, "so_exp"])
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    pr = ctx.Process(target=_inject_worker, args=(q, where))
+    pr.start()
+    r = q.get(timeout=500)
+    pr.join(timeout=60)
+    assert "error" not in r, r.get("error")
+    assert r == {"failed": True, "code_not_param": True, "wrapper_dropped": True, "then_refused": True,
+                 "after_equal": True}, r
