@@ -150,6 +150,41 @@ int lzma_enc_batch(lzma_ctx *ctx, const lzma_params *p,
 int lzma_encode(lzma_ctx *ctx, const lzma_params *p, const uint8_t *in, uint64_t n,
                 uint8_t *out, uint64_t out_cap, uint64_t *out_len);
 
+/* ---- the sliced encode: ONE long stream in bounded device launches ------
+ * Encoder.Code (Encoder.java:1064-1077) over one stream, the parse and range coder run a
+ * slice at a time: every launch stops at the first CodeOneBlock boundary
+ * (Encoder.java:843-936; no look-ahead pending) past its stop position, with the
+ * encoder's state (models, price tables and their refresh countdowns, reps, the range
+ * coder's low / range / cache) kept in HBM for the next launch. The bytes are exactly
+ * lzma_encode's. What it is for: a single serial parse of a 1 GiB stream is one ~30-minute
+ * kernel; slices bound every launch (watchdogs, preemption), report progress between them
+ * (ICodeProgress.SetProgress, Encoder.java:1070-1072, at block granularity instead of once
+ * at the end), and checkpoint to the host so another process can finish the stream.
+ *   lzma_enc_session_begin: d_in[0 .. n) device-resident, n < 2^31; d_out of at least
+ *     lzma_enc_bound(n) bytes, both valid until _end. Runs the match finder over the whole
+ *     stream (it is a pure function of the input, so a restored session recomputes it).
+ *     While the session is open the context's other encode / decode / pack entry points
+ *     return LZMA_E_PARAM.
+ *   lzma_enc_session_step: parses and codes at least `bytes` more input (a slice ends at
+ *     the next block boundary, within 4 KiB + 273 bytes past that) and appends the slice's
+ *     final output bytes at d_out[*out_len ..]; *in_pos = input consumed, *out_len = output
+ *     bytes final so far, *done = 1 once the stream is flushed (then a no-op).
+ *   lzma_enc_session_save: the state after the last step as a blob (blob NULL: *len =
+ *     the size needed): parameters, positions, coder state, the parser state (~6 KiB plus
+ *     the literal coders, 12 KiB at lc 3).
+ *   lzma_enc_session_restore: on a fresh session over the same input and parameters
+ *     (before its first step): go on from the blob; the caller keeps the first *out_len
+ *     output bytes (they are final) and the session writes after them.
+ * No reference counterpart beyond Encoder.Code itself (the Java encoder keeps its state
+ * in the Encoder instance between CodeOneBlock calls, Encoder.java:843-936). */
+typedef struct lzma_enc_session lzma_enc_session;
+int lzma_enc_session_begin(lzma_ctx *ctx, const lzma_params *p, const uint8_t *d_in, uint64_t n,
+                           uint8_t *d_out, uint64_t out_cap, void *hip_stream, lzma_enc_session **out);
+int lzma_enc_session_step(lzma_enc_session *s, uint64_t bytes, uint64_t *in_pos, uint64_t *out_len, int *done);
+int lzma_enc_session_save(const lzma_enc_session *s, uint8_t *blob, uint64_t cap, uint64_t *len);
+int lzma_enc_session_restore(lzma_enc_session *s, const uint8_t *blob, uint64_t len);
+void lzma_enc_session_end(lzma_enc_session *s);
+
 /* ---- decode -------------------------------------------------------------
  * props: the 5 property bytes (Decoder.SetDecoderProperties).
  * h_out_sizes[i] = outSize of Decoder.Code (-1 => until end marker).

@@ -33,7 +33,18 @@
 
 #include <type_traits>
 
+// LZG_ENC_SLICED (enc_slice.hip): the same parser, compiled once more with the stop / resume
+// of the sliced encode (lzma_enc_session_*) into namespace lzg::sliced. The product kernels
+// of the batch encode keep their code and register allocation: the slicing is not in them.
+#ifndef LZG_ENC_SLICED
+#define LZG_ENC_SLICED 0
+#endif
+
 namespace lzg {
+#if LZG_ENC_SLICED
+namespace sliced {
+#endif
+constexpr bool kSliced = LZG_ENC_SLICED != 0;
 
 static __constant__ Tables c_tab = make_tables();
 
@@ -141,6 +152,22 @@ FI uint32_t sel4(uint32_t i, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
 // FairPrio rows of the encoder's waves (lzma_common.h)
 __device__ uint32_t g_enc_sched[kSchedRows * kSchedCols];
 
+// The sliced encode's per-stream parser state in HBM (lzma_enc_session_*): everything of
+// Encoder's that a CodeOneBlock boundary (Encoder.java:843-936, _additionalOffset == 0: no
+// look-ahead pending, the _optimum path consumed) carries to the next block: the scalars
+// (SS_* words), the probability models, the length-price tables with their countdowns and
+// the distance / align price tables as last refreshed (the refresh schedule decides the
+// output, so they are saved, not recomputed), and the literal coders. The decision-price
+// cache (dmp) is a function of the models and is rebuilt.
+enum { SL_SCALARS, SL_PROBS, SL_LENP, SL_LENC, SL_PSP, SL_DP, SL_AP, SL_LIT, SL_COUNT };
+__host__ __device__ constexpr uint32_t slice_layout(uint32_t pb, uint32_t lc, uint32_t lp, uint32_t tsize, uint32_t* off) {
+    const uint32_t sz[SL_COUNT] = {SS_WORDS * 4, prob_count(pb) * 2, 2 * (1u << pb) * tsize * 2, 2 * 16 * 4, 256 * 2,
+                                   512 * 2, 16 * 4, (0x300u << (lc + lp)) * 2};
+    uint32_t o = 0;
+    for (int i = 0; i < SL_COUNT; i++) { if (off) off[i] = o; o += (sz[i] + 15) & ~15u; }
+    return o;
+}
+
 template <typename PairT, bool LIT_LDS, int PBS, bool RING>
 struct Enc {
     using PP = PairPack<PairT>;
@@ -226,6 +253,9 @@ struct Enc {
         FairPrio prio;
     };
     Cold* cold;
+    // ---- the sliced encode (kSliced kernels only): the stream's state region, where to stop
+    uint8_t* sst;
+    uint32_t sstop, sresume;
     // ---- per-position gather (see gather()): p = current position, equality masks per side
     uint32_t gp;
     // RING (fb <= 32): 32-bit masks, bit k = offset k (0 .. 31), enough for every length up
@@ -1511,6 +1541,74 @@ struct Enc {
     FI void flush(uint32_t now_pos) {   // the coder's own flush (5 x ShiftLow) runs in rc.hip
         if (eos) encode_symbol(0, kMatchMinLen, now_pos, prev_byte, 0, true);
         rec_store_tail();
+        if constexpr (kSliced) save_state(now_pos, 1);   // the stream is done (the host reads SS_DONE)
+    }
+
+    // ------------------------------------------------------------ the sliced encode's state
+    // (kSliced kernels; the layout is slice_layout). Every lane copies its share of each table;
+    // the scalars go through one lane-indexed store per word (vector stores).
+    FI uint32_t slice_scalar(uint32_t k, uint32_t now_pos, uint32_t done) const {
+        const uint32_t v[SS_WORDS] = {kSliceMagic, now_pos, done, state, prev_byte, rd0, rd1, rd2, rd3,
+                                      match_price_count, align_price_count, 0u, 0u, 0u, 0u, 0u};
+        uint32_t r = 0;
+#pragma unroll
+        for (int i = 0; i < SS_WORDS; i++) r = k == (uint32_t)i ? v[i] : r;
+        return r;
+    }
+    FI void save_state(uint32_t now_pos, uint32_t done) {
+        uint32_t off[SL_COUNT];
+        slice_layout(pb, lc, lp, tsize, off);
+        const uint32_t nlit = 0x300u << (lc + lp);
+        uint32_t* sc = (uint32_t*)(sst + off[SL_SCALARS]);
+        LANE_FOR(uint32_t, k, 0u, (uint32_t)SS_WORDS) sc[k] = slice_scalar(k, now_pos, done);
+        if (done) return;   // a finished stream needs no tables
+        uint16_t* g16 = (uint16_t*)(sst + off[SL_PROBS]);
+        LANE_FOR(uint32_t, i, 0u, (uint32_t)E_COUNT) g16[i] = probs[i];
+        g16 = (uint16_t*)(sst + off[SL_LENP]);
+        LANE_FOR(uint32_t, i, 0u, (2u << pb) * tsize) g16[i] = lenp[i];
+        uint32_t* g32 = (uint32_t*)(sst + off[SL_LENC]);
+        LANE_FOR(uint32_t, i, 0u, 32u) g32[i] = lenc[i];
+        g16 = (uint16_t*)(sst + off[SL_PSP]);
+        LANE_FOR(uint32_t, i, 0u, 256u) g16[i] = psp[i];
+        g16 = (uint16_t*)(sst + off[SL_DP]);
+        LANE_FOR(uint32_t, i, 0u, 512u) g16[i] = dp[i];
+        g32 = (uint32_t*)(sst + off[SL_AP]);
+        LANE_FOR(uint32_t, i, 0u, 16u) g32[i] = ap[i];
+        if (!LIT_LDS) SPILL_FENCE();   // the coders' last HBM stores before they are copied
+        g16 = (uint16_t*)(sst + off[SL_LIT]);
+        LANE_FOR(uint32_t, i, 0u, nlit) g16[i] = lit[i];
+    }
+    // returns now_pos; every Encoder field a CodeOneBlock boundary carries, as saved
+    FI uint32_t load_state() {
+        uint32_t off[SL_COUNT];
+        slice_layout(pb, lc, lp, tsize, off);
+        const uint32_t nlit = 0x300u << (lc + lp);
+        const uint16_t* g16 = (const uint16_t*)(sst + off[SL_PROBS]);
+        LANE_FOR(uint32_t, i, 0u, (uint32_t)E_COUNT) probs[i] = g16[i];
+        g16 = (const uint16_t*)(sst + off[SL_LENP]);
+        LANE_FOR(uint32_t, i, 0u, (2u << pb) * tsize) lenp[i] = g16[i];
+        const uint32_t* g32 = (const uint32_t*)(sst + off[SL_LENC]);
+        LANE_FOR(uint32_t, i, 0u, 32u) lenc[i] = g32[i];
+        g16 = (const uint16_t*)(sst + off[SL_PSP]);
+        LANE_FOR(uint32_t, i, 0u, 256u) psp[i] = g16[i];
+        g16 = (const uint16_t*)(sst + off[SL_DP]);
+        LANE_FOR(uint32_t, i, 0u, 512u) dp[i] = g16[i];
+        g32 = (const uint32_t*)(sst + off[SL_AP]);
+        LANE_FOR(uint32_t, i, 0u, 16u) ap[i] = g32[i];
+        g16 = (const uint16_t*)(sst + off[SL_LIT]);
+        LANE_FOR(uint32_t, i, 0u, nlit) lit[i] = g16[i];
+        if (!LIT_LDS) SPILL_FENCE();
+        LANE_FENCE();
+        LANE_FOR(uint32_t, i, 0u, (uint32_t)E_PSLOT) dmp[i] = price0(probs[i]) | (price1(probs[i]) << 16);
+        LANE_FENCE();
+        const uint32_t* sc = (const uint32_t*)(sst + off[SL_SCALARS]);
+        const uint32_t now_pos = uni32(sc[SS_NOW_POS]);
+        state = uni32(sc[SS_STATE]); prev_byte = uni32(sc[SS_PREV_BYTE]);
+        rd0 = uni32(sc[SS_REP0]); rd1 = uni32(sc[SS_REP1]); rd2 = uni32(sc[SS_REP2]); rd3 = uni32(sc[SS_REP3]);
+        match_price_count = uni32(sc[SS_MATCH_PRICE_COUNT]); align_price_count = uni32(sc[SS_ALIGN_PRICE_COUNT]);
+        if (uni32(sc[SS_MAGIC]) != kSliceMagic || now_pos == 0 || now_pos >= n) bad = 10;
+        mfpos = now_pos;
+        return now_pos;
     }
 
     FI void run() {   // Encoder.Code: SetStreams + CodeOneBlock/encodeOne (Encoder.java:843-936, 1046-1077)
@@ -1518,6 +1616,18 @@ struct Enc {
         for (int k = 0; k < kProfSlots; k++) prof[k] = 0;
 #endif
         const uint32_t nlit = 0x300u << (lc + lp);
+        rp0 = rp1 = rp2 = rp3 = 0;
+        rpos = 0; overflow = 0; bad = 0;
+        longest_found = 0; opt_end = 0; opt_cur = 0; additional_offset = 0;
+        longest_len = 0; num_pairs = 0; mfpos = 0;
+        ring_base = 0x80000000u;   // force a fill at the first read (streams < 2 GiB)
+        uint32_t now_pos = 0;
+        bool resumed = false;
+        if constexpr (kSliced) resumed = sresume != 0;
+        if (resumed) {   // the sliced encode: a CodeOneBlock boundary of an earlier launch
+            now_pos = load_state();
+            if (bad) return;
+        } else {
         LANE_FOR(uint32_t, i, 0u, (uint32_t)E_COUNT) probs[i] = kBitModelTotal >> 1;
         LANE_FOR(uint32_t, i, 0u, (uint32_t)E_PSLOT) dmp[i] = price0(kBitModelTotal >> 1) | (price1(kBitModelTotal >> 1) << 16);
         LANE_FOR(uint32_t, i, 0u, nlit) lit[i] = kBitModelTotal >> 1;
@@ -1526,11 +1636,6 @@ struct Enc {
         LANE_FENCE();
         state = 0; prev_byte = 0;
         rd0 = rd1 = rd2 = rd3 = 0;
-        rp0 = rp1 = rp2 = rp3 = 0;
-        rpos = 0; overflow = 0; bad = 0;
-        longest_found = 0; opt_end = 0; opt_cur = 0; additional_offset = 0;
-        longest_len = 0; num_pairs = 0; mfpos = 0;
-        ring_base = 0x80000000u;   // force a fill at the first read (streams < 2 GiB)
         match_price_count = 0; align_price_count = 0;
         DBG(1, 1);
         fill_distances_prices();
@@ -1539,9 +1644,10 @@ struct Enc {
         DBG(1, 3);
         for (uint32_t ps = 0; ps < (1u << pb); ps++) { update_len_table(0, ps); update_len_table(1, ps); }
         DBG(1, 4);
+        }
 
-        uint32_t now_pos = 0;
         cold->prio.start(g_enc_sched, n, lane_id());
+        if (!resumed) {
         if (avail() == 0) { flush(0); return; }
         read_match_distances();
         DBG(1, 5);
@@ -1549,6 +1655,7 @@ struct Enc {
         additional_offset--;
         now_pos++;
         if (avail() == 0) { flush(now_pos); return; }
+        }
         DBG(1, 6);
         for (;;) {
             int32_t back;
@@ -1591,6 +1698,9 @@ struct Enc {
                 PEND(PF_TABLES, tt);
                 cold->prio.update(now_pos, lane_id());
                 if (avail() == 0) { flush(now_pos); return; }
+                if constexpr (kSliced) {   // a slice ends at the first block boundary past its stop
+                    if (now_pos >= sstop) { rec_store_tail(); save_state(now_pos, 0); return; }
+                }
             }
         }
     }
@@ -1697,6 +1807,11 @@ __global__ void __launch_bounds__(kWave, 4) enc_kernel(EncArgs a) {
     e.n = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(uni64(a.offs[s + 1]) - e.gbase));
     e.in = a.in + e.gbase;
     e.inb = __builtin_amdgcn_make_buffer_rsrc((void*)e.in, 0, e.n, 0x00020000);
+    if constexpr (kSliced) {   // the stream's own state region
+        e.sst = a.slice_state + (size_t)s * a.slice_stride;
+        e.sstop = a.slice_stop;
+        e.sresume = a.slice_resume;
+    }
     const uint64_t ro = uni64(a.rec_offs[s]);
     e.recs = a.recs + ro;
     e.rcap = uni64(a.rec_offs[s + 1]) - ro;
@@ -1726,6 +1841,7 @@ __global__ void __launch_bounds__(kWave, 4) enc_kernel(EncArgs a) {
     }
 }
 
+#if !LZG_ENC_SLICED   // shared by both parsers: defined once, in the plain one's translation unit
 size_t enc_lds_bytes(const EncArgs& a) { return enc_lds_layout(a, nullptr); }
 
 size_t enc_scratch_per_block(const Derived&) { return (size_t)kNumOpts * 4 * 10 + 256; }
@@ -1741,6 +1857,7 @@ uint32_t enc_lit_in_lds(const Derived& d, int nstreams) {
 }
 
 int enc_grid(const Derived&, int nstreams) { return nstreams; }   // one workgroup per stream
+#endif
 
 template <typename PairT, bool LIT, int PBS, int SPEC>
 static void launch_spec(Ctx* ctx, const EncArgs& a, int grid, size_t lds, hipStream_t st) {
@@ -1794,4 +1911,15 @@ int launch_encoder(Ctx* ctx, const EncArgs& a0, bool wide_pairs, int grid, hipSt
     return LZMA_OK;
 }
 
+#if LZG_ENC_SLICED
+}  // namespace sliced
+
+int launch_encoder_sliced(Ctx* ctx, const EncArgs& a, bool wide_pairs, int grid, hipStream_t st) {
+    if (!a.slice_state) return ctx->fail(LZMA_E_INTERNAL, "sliced encode without a state region");
+    return sliced::launch_encoder(ctx, a, wide_pairs, grid, st);
+}
+size_t enc_slice_state_bytes(const Derived& d) {
+    return sliced::slice_layout(d.pb, d.lc, d.lp, d.len_table_size, nullptr);
+}
+#endif
 }  // namespace lzg

@@ -126,7 +126,14 @@ __device__ __forceinline__ uint32_t rec_at(const uint32_t (&w)[32], int k) {
 // add into the next segment's first bytes; carries run toward the stream start.
 // 128-record multiples: a segment's staged bytes (at most records + 1, plus the ring's
 // 72-byte write-back past them) then stay inside its own 2-byte-per-record region
-__device__ __forceinline__ uint64_t rc_seglen(uint64_t n) {
+// The sliced encode (RcArgs::sliced) cuts differently: the coder's end state after a slice
+// is the end state of its last non-empty segment only if no earlier segment's unfinished
+// digits reach that segment's own unfinished digits. Below 2^20 records a slice is one
+// segment (segments 1.. are empty); above, the splits round down, so the last segment holds
+// at least n / 16 >= 65536 records and emits far more than the 5 digits an earlier
+// segment's tail adds into its first bytes (rc_merge_kernel checks it).
+__device__ __forceinline__ uint64_t rc_seglen(uint64_t n, bool sliced = false) {
+    if (sliced) return n < (1u << 20) ? (n ? n : 1) : (n / (128 * kRcSegs)) * 128;
     return ((n + 128 * kRcSegs - 1) / (128 * kRcSegs)) * 128;
 }
 __device__ __forceinline__ uint64_t rc_split(uint64_t n, uint64_t seglen, int k) {
@@ -140,11 +147,11 @@ __global__ void __launch_bounds__(kRcLanes) rc_range_kernel(RcArgs a) {
     if (i >= a.nstreams) return;
     const uint32_t s = a.order[i];
     if (a.status[s] != LZMA_OK) return;
-    const uint64_t n = a.rec_lens[s], seglen = rc_seglen(n);
+    const uint64_t n = a.rec_lens[s], seglen = rc_seglen(n, a.sliced);
     const uint32_t* r32 = (const uint32_t*)(a.recs + a.rec_offs[s]);
     uint32_t* seg = a.seg + (size_t)s * kRcSegs * kRcSegWords;
     const uint64_t need = rc_split(n, seglen, kRcSegs - 1);   // records before the last split
-    uint32_t range = 0xFFFFFFFFu;
+    uint32_t range = a.init_state ? a.init_state[(size_t)s * kRcStateWords] : 0xFFFFFFFFu;
     seg[0] = range;
     int next = 1;                                            // next split to record
     // Encode / EncodeDirectBits, range only. bit ? range - t*p : t*p (t = range >> 11) is one
@@ -196,7 +203,7 @@ __global__ void __launch_bounds__(kRcLanes) rc_kernel(RcArgs a) {
     const uint32_t s = a.order[i / kRcSegs];
     const int sk = i % kRcSegs;
     if (a.status[s] != LZMA_OK) return;
-    const uint64_t nall = a.rec_lens[s], seglen = rc_seglen(nall);
+    const uint64_t nall = a.rec_lens[s], seglen = rc_seglen(nall, a.sliced);
     const uint64_t r0 = rc_split(nall, seglen, sk);
     const uint64_t n = (sk + 1 < kRcSegs ? rc_split(nall, seglen, sk + 1) : nall) - r0;
     uint16_t* region = a.recs + a.rec_offs[s] + r0;   // 64-record (128-byte) aligned
@@ -210,6 +217,10 @@ __global__ void __launch_bounds__(kRcLanes) rc_kernel(RcArgs a) {
     c.outpos = 0;
     c.tailw = 0;
     c.lo = 0; c.carry = 0; c.range = seg[0]; c.cache = 0; c.cache_size = 1;   // Init (:18-24) at the segment's range
+    if (sk == 0 && a.init_state) {   // a slice of a longer stream: the coder where the last slice left it
+        const uint32_t* is = a.init_state + (size_t)s * kRcStateWords;
+        c.lo = is[1]; c.carry = is[2]; c.cache = is[3]; c.cache_size = is[4];
+    }
     // blocks of 64 records (32 dwords per lane); the next block's loads are issued
     // before this block is coded, so their HBM latency overlaps the coding
     const uint64_t nblk = (n + 63) >> 6, full = n >> 6;
@@ -255,11 +266,11 @@ __global__ void __launch_bounds__(kRcLanes) rc_kernel(RcArgs a) {
 #pragma unroll
         for (int j = 0; j < 32; j++) cur[j] = nxt[j];
     }
-    if (sk == kRcSegs - 1) {
+    if (sk == kRcSegs - 1 && a.flush) {
 #pragma unroll 1
         for (int k = 0; k < 5; k++) c.shift_low();   // FlushData (:31-36)
     }
-    seg[1] = c.outpos; seg[2] = c.lo; seg[3] = c.carry; seg[4] = c.cache; seg[5] = c.cache_size;
+    seg[1] = c.outpos; seg[2] = c.lo; seg[3] = c.carry; seg[4] = c.cache; seg[5] = c.cache_size; seg[6] = c.range;
 }
 
 // the segments of a stream into the caller's output layout (one workgroup per stream):
@@ -269,14 +280,24 @@ __global__ void __launch_bounds__(256) rc_merge_kernel(RcArgs a) {
     const uint32_t s = blockIdx.x;
     if (a.status[s] != LZMA_OK) return;
     const uint32_t* seg = a.seg + (size_t)s * kRcSegs * kRcSegWords;
-    const uint64_t nall = a.rec_lens[s], seglen = rc_seglen(nall);
+    const uint64_t nall = a.rec_lens[s], seglen = rc_seglen(nall, a.sliced);
     uint64_t pos[kRcSegs + 1];
     pos[0] = 0;
     for (int k = 0; k < kRcSegs; k++) {
         const uint32_t* g = seg + k * kRcSegWords;
         pos[k + 1] = pos[k] + g[1] + g[5] - 1;
     }
-    const uint64_t total = pos[kRcSegs - 1] + seg[(kRcSegs - 1) * kRcSegWords + 1];
+    // an unflushed slice (the sliced encode): its output ends with the last non-empty
+    // segment's emitted bytes; that segment's unfinished digits and end range are the
+    // coder's state for the next slice (rc_seglen)
+    const int last = (a.sliced && !a.flush) ? (seglen >= nall ? 0 : kRcSegs - 1) : kRcSegs - 1;
+    const uint64_t total = pos[last] + seg[last * kRcSegWords + 1];
+    if (a.sliced && !a.flush && threadIdx.x == 0) {
+        const uint32_t* g = seg + last * kRcSegWords;
+        uint32_t* es = a.end_state + (size_t)s * kRcStateWords;
+        es[0] = g[6]; es[1] = g[2]; es[2] = g[3]; es[3] = g[4]; es[4] = g[5];
+        if (last > 0 && g[1] < 5) a.status[s] = LZMA_E_INTERNAL;   // an earlier tail would reach its digits (rc_seglen)
+    }
     const uint64_t cap = a.out_offs[s + 1] - a.out_offs[s];
     if (threadIdx.x == 0) a.out_lens[s] = total;
     if (total > cap) {
@@ -284,15 +305,15 @@ __global__ void __launch_bounds__(256) rc_merge_kernel(RcArgs a) {
         return;
     }
     uint8_t* dst = a.out + a.out_offs[s];
-    for (int k = 0; k < kRcSegs; k++) {
+    for (int k = 0; k <= last; k++) {
         const uint8_t* src = (const uint8_t*)(a.recs + a.rec_offs[s] + rc_split(nall, seglen, k));
         const uint32_t len = seg[k * kRcSegWords + 1];
-        const uint64_t end = k + 1 < kRcSegs ? pos[k + 1] : total;   // the pending digits start as 0
+        const uint64_t end = k < last ? pos[k + 1] : total;   // the pending digits start as 0
         for (uint64_t j = threadIdx.x; j < end - pos[k]; j += blockDim.x) dst[pos[k] + j] = j < len ? src[j] : 0;
     }
     __syncthreads();
     if (threadIdx.x != 0) return;
-    for (int k = 0; k + 1 < kRcSegs; k++) {
+    for (int k = 0; k < last; k++) {
         const uint32_t* g = seg + k * kRcSegWords;
         const uint32_t len = g[1], lo = g[2], cy = g[3], cache = g[4], cs = g[5];
         const uint64_t q0 = pos[k] + len;   // the cache digit

@@ -185,6 +185,9 @@ struct Ctx {
     hipStream_t walk_stream = nullptr;     // a staged pass's walk beside the older pass's parse
     DevBuf split_recs[2], split_coder[2];  // per coder set: the coder records and per-stream arrays (apart from the arena)
     HostBuf pin_rc[2];                     // per slot: the coder's lengths and verdicts, written by the device
+    // an open sliced encode (lzma_enc_session_*) holds the live slot and the arena: the
+    // context's other encode, decode and pack entry points refuse while it is open
+    struct EncSession* session = nullptr;
     // timing
     bool timing = false;
     struct Pending { std::string name; hipEvent_t a, b; };
@@ -385,6 +388,12 @@ struct EncArgs {
     uint32_t fb, lc, lp, pb, eos, dist_table_size, len_table_size;
     uint32_t lit_in_lds;
     uint32_t pair_bytes;          // 4 (u32 packed pairs) or 8 (u64, streams >= 8 MiB)
+    // the sliced encode (lzma_enc_session_*, the LZG_ENC_SLICED kernels): per-stream parser state
+    // in HBM (enc.hip slice_layout), a parse that stops at the first CodeOneBlock boundary
+    // (additional_offset == 0) with now_pos >= slice_stop, or resumes from the saved state
+    uint8_t* slice_state;
+    uint64_t slice_stride;
+    uint32_t slice_stop, slice_resume;
     uint32_t* dbg;                // debug checkpoints (host-mapped, LZMA_MI355X_DEBUG only) or null
     uint64_t* prof;               // phase cycles [nstreams][kProfSlots] (LZG_PROF builds) or null
 };
@@ -394,6 +403,14 @@ enum { PF_TOTAL, PF_GETOPT, PF_MATCHES, PF_REPLEN, PF_TWOLEN, PF_LIT, PF_RELAX, 
        PF_ENCODE, PF_TABLES, PF_NOPT, PF_NPOS, PF_NSPILL, PF_NOVF, PF_NTWO, PF_T0, PF_T1, PF_HWID, kProfSlots };
 
 int launch_encoder(Ctx* ctx, const EncArgs& a, bool wide_pairs, int grid, hipStream_t st);
+// enc_slice.hip: the same parser compiled with LZG_ENC_SLICED (stop / resume at CodeOneBlock
+// boundaries); the per-stream state size for these parameters
+int launch_encoder_sliced(Ctx* ctx, const EncArgs& a, bool wide_pairs, int grid, hipStream_t st);
+size_t enc_slice_state_bytes(const Derived& d);
+// scalar words at the front of a stream's slice state (enc.hip), readable by the host
+enum { SS_MAGIC, SS_NOW_POS, SS_DONE, SS_STATE, SS_PREV_BYTE, SS_REP0, SS_REP1, SS_REP2, SS_REP3, SS_MATCH_PRICE_COUNT,
+       SS_ALIGN_PRICE_COUNT, SS_WORDS = 16 };
+constexpr uint32_t kSliceMagic = 0x534C5A4Cu;   // "LZLS"
 
 // rc.hip: the range coder over the parser's records, one lane per stream
 struct RcArgs {
@@ -406,8 +423,18 @@ struct RcArgs {
     uint8_t* out;
     const uint64_t* out_offs;     // output capacity layout (nstreams+1)
     uint64_t* out_lens;
-    uint32_t* seg;                // [nstreams][kRcSegs][kRcSegWords]: start range, bytes, lo, carry, cache, cache size
+    uint32_t* seg;                // [nstreams][kRcSegs][kRcSegWords]: start range, bytes, lo, carry, cache, cache size,
+                                  // end range
+    // The sliced encode (lzma_enc_session_*): a stream's records arrive slice by slice and the
+    // coder carries its state from one slice to the next. sliced: segment 0 starts from
+    // init_state (null: Init), the segments are cut so the last non-empty one holds the coder's
+    // end state (rc_seglen), and without `flush` the unfinished digits stay out of the output
+    // and the end state goes to end_state. State words: range, lo, carry, cache, cache size.
+    uint32_t sliced, flush;
+    const uint32_t* init_state;   // [nstreams][kRcStateWords] or null
+    uint32_t* end_state;          // [nstreams][kRcStateWords] or null
 };
+constexpr int kRcStateWords = 8;
 constexpr int kRcSegs = 16;       // coder segments per stream (rc.hip)
 constexpr int kRcSegWords = 8;
 int launch_rc(Ctx* ctx, const RcArgs& a, hipStream_t st);

@@ -136,6 +136,9 @@ struct EncPass {
     int32_t* d_status = nullptr;
     unsigned* d_next = nullptr;
     uint16_t* d_recs = nullptr;
+    // the sliced encode (lzma_enc_session_*): the parse stops / resumes at block boundaries
+    uint8_t* slice_state = nullptr;
+    uint32_t slice_stop = 0, slice_resume = 0;
     uint64_t pool_cap(uint64_t spk) const {   // one slot per position at most
         uint64_t slots = std::min<uint64_t>(total, (total * spk + 1023) / 1024) + 64;
         return slots * stride;
@@ -368,7 +371,16 @@ static int pass_parse(Ctx* ctx, EncPass& P, hipStream_t st) {
             return ctx->fail(LZMA_E_DEVICE, "parse event");
         HIPCHK(hipEventRecord(ctx->parse_start, st));
     }
-    int rc = launch_encoder(ctx, a, P.wide, P.grid, st);
+    int rc;
+    if (P.slice_state) {
+        a.slice_state = P.slice_state;
+        a.slice_stride = 0;   // one stream
+        a.slice_stop = P.slice_stop;
+        a.slice_resume = P.slice_resume;
+        rc = launch_encoder_sliced(ctx, a, P.wide, P.grid, st);
+    } else {
+        rc = launch_encoder(ctx, a, P.wide, P.grid, st);
+    }
     if (rc) return rc;
     LZG_TRACE(ctx, st, "enc_parse done");
     watch.stop();
@@ -382,8 +394,10 @@ static int pass_parse(Ctx* ctx, EncPass& P, hipStream_t st) {
 // the range coder over the parser's records (the coder's arrays: the pass's own, or the
 // split form's copies)
 static int pass_rc(Ctx* ctx, EncPass& P, uint64_t* rofs, uint64_t* rlens, uint32_t* order, int32_t* status, uint64_t* oofs,
-                   uint64_t* lens, uint32_t* seg, hipStream_t st) {
+                   uint64_t* lens, uint32_t* seg, hipStream_t st, const RcArgs* slice = nullptr) {
     RcArgs ra{};
+    if (slice) ra = *slice;   // the sliced encode's coder state and flush (sliced, flush, init_state, end_state)
+    else ra.flush = 1;
     ra.recs = P.d_recs; ra.rec_offs = rofs; ra.rec_lens = rlens; ra.order = order; ra.nstreams = P.ns;
     ra.status = status; ra.out = P.d_out; ra.out_offs = oofs; ra.out_lens = lens; ra.seg = seg;
     int rc = launch_rc(ctx, ra, st);
@@ -399,6 +413,7 @@ static int encode_pass(Ctx* ctx, const Derived& d, const uint8_t* d_in, const ui
     if (ctx->dec_pending) return ctx->fail(LZMA_E_PARAM, "an asynchronous decode is in flight: lzma_dec_batch_dev_wait first");
     if (ctx->split_state || ctx->rc_pending)
         return ctx->fail(LZMA_E_PARAM, "a split encode is in flight on this context: lzma_enc_parse_dev_async / _wait first");
+    if (ctx->session) return ctx->fail(LZMA_E_PARAM, "an encode session is open on this context: lzma_enc_session_end first");
     EncPass P;
     pass_plan(ctx, P, d, d_in, h_offs, s0, s1, d_out, h_out_offs, false);
     // Nothing is staged, so either live slot is free: take the larger one. A split schedule
@@ -546,6 +561,7 @@ static int enc_stage_dev(Ctx* ctx, const lzma_params* p, const uint8_t* d_in, co
                          uint8_t* d_out, const uint64_t* h_out_offs, hipStream_t st) {
     if (ctx->dec_pending) return ctx->fail(LZMA_E_PARAM, "an asynchronous decode is in flight: lzma_dec_batch_dev_wait first");
     if (ctx->split_state >= 2) return ctx->fail(LZMA_E_PARAM, "two batches are already staged: lzma_enc_parse_dev_async first");
+    if (ctx->session) return ctx->fail(LZMA_E_PARAM, "an encode session is open on this context: lzma_enc_session_end first");
     Derived d;
     if (derive(*p, d) != LZMA_OK) return ctx->fail(LZMA_E_PARAM, "invalid lzma_params");
     if (nstreams <= 0) return ctx->fail(LZMA_E_PARAM, "the split form needs at least one stream");
@@ -790,6 +806,7 @@ static int decode_batch_dev_async(Ctx* ctx, const uint8_t props[5], const uint8_
     if (ctx->dec_pending) return ctx->fail(LZMA_E_PARAM, "an asynchronous decode is already in flight on this context");
     if (ctx->split_state || ctx->rc_pending)   // the decode carves the arena the staged pass holds
         return ctx->fail(LZMA_E_PARAM, "a split encode is in flight on this context: lzma_enc_parse_dev_async / _wait first");
+    if (ctx->session) return ctx->fail(LZMA_E_PARAM, "an encode session is open on this context: lzma_enc_session_end first");
     if (nstreams <= 0) return nstreams == 0 ? LZMA_OK : ctx->fail(LZMA_E_PARAM, "nstreams < 0");
     const size_t n = (size_t)nstreams;
     const size_t words = (n + 1) * 3 + n + (n + 1) / 2 * 2 + 2;   // in_offs, sizes, out_offs, lens, order + status
@@ -842,6 +859,171 @@ static int decode_batch_dev_wait(Ctx* ctx, uint64_t* h_out_lens, int32_t* h_stat
     }
     if (h_out_lens) memcpy(h_out_lens, lens, n * 8);
     if (h_status) memcpy(h_status, status, n * 4);
+    return LZMA_OK;
+}
+
+// ---- the sliced encode (lzma_enc_session_*): one stream encoded in bounded launches
+// begin: the stream's match finder over the whole input (match lists are a pure function of
+// the input); step: the parser from the saved state up to the first CodeOneBlock
+// boundary past the stop (enc_slice.hip), then the range coder over that slice's records from
+// the coder state the last slice left (rc.hip, RcArgs::sliced), its final bytes appended to
+// the output; save / restore: the state between steps as a host blob, so a later process can
+// go on (the caller keeps the output written so far).
+constexpr uint32_t kSessMagic = 0x53455A4Cu;   // "LZES"
+constexpr uint32_t kBlobMagic = 0x42455A4Cu;   // "LZEB"
+struct EncSession {
+    uint32_t magic = kSessMagic;
+    Ctx* ctx = nullptr;
+    EncPass P;
+    lzma_params params{};
+    hipStream_t st = nullptr;
+    uint8_t* d_state = nullptr;    // the parser's slice state (enc_slice_state_bytes)
+    uint32_t* d_rc = nullptr;      // the coder's state between slices (kRcStateWords)
+    size_t state_bytes = 0;
+    uint64_t n = 0, in_pos = 0, out_len = 0, out_cap = 0;
+    int done = 0, steps = 0;
+};
+static bool ok_sess(const EncSession* s) { return s && s->magic == kSessMagic && s->ctx; }
+
+// the blob: a header of u64 words, then the parser state (absent once the stream is done)
+enum { B_MAGIC, B_VERSION, B_DICT, B_FB, B_MF, B_LCLPPB, B_EOS, B_N, B_IN_POS, B_OUT_LEN, B_DONE, B_STATE_BYTES,
+       B_RC, B_WORDS = B_RC + kRcStateWords / 2 };
+
+static void session_free(EncSession* S) {
+    if (S->d_state) hipFree(S->d_state);
+    if (S->d_rc) hipFree(S->d_rc);
+    S->d_state = nullptr;
+    S->d_rc = nullptr;
+}
+
+static int session_begin(Ctx* ctx, const lzma_params* p, const uint8_t* d_in, uint64_t n, uint8_t* d_out, uint64_t out_cap,
+                         hipStream_t st, EncSession** out) {
+    if (ctx->dec_pending || ctx->split_state || ctx->rc_pending || ctx->session)
+        return ctx->fail(LZMA_E_PARAM, "the context is busy (a decode, split encode or session in flight)");
+    Derived d;
+    if (derive(*p, d) != LZMA_OK) return ctx->fail(LZMA_E_PARAM, "invalid lzma_params");
+    if (n >= (1ull << 31)) return ctx->fail(LZMA_E_PARAM, "stream >= 2 GiB");
+    if (out_cap < lzma_enc_bound(n)) return ctx->fail(LZMA_E_PARAM, "out_cap below lzma_enc_bound(n)");
+    EncSession* S = new (std::nothrow) EncSession;
+    if (!S) return ctx->fail(LZMA_E_NOMEM, "session");
+    S->ctx = ctx; S->params = *p; S->st = st; S->n = n; S->out_cap = out_cap;
+    const uint64_t offs[2] = {0, n}, oofs[2] = {0, out_cap};
+    EncPass& P = S->P;
+    pass_plan(ctx, P, d, d_in, offs, 0, 1, d_out, oofs, false);
+    P.slot = ctx->live[1].n > ctx->live[0].n ? 1 : 0;
+    int rc;
+    if ((rc = pass_carve(ctx, P)) || (rc = pass_stage(ctx, P, st)) ||
+        (rc = mf_front(ctx, P.d, P.inpad, P.d_offs, P.ns, P.total, P.wide, P.w, st)) || (rc = pass_mf_back(ctx, P, st))) {
+        delete S;
+        return rc;
+    }
+    S->state_bytes = enc_slice_state_bytes(d);
+    ctx->count_alloc(S->state_bytes + kRcStateWords * 4);
+    if (hipMalloc(&S->d_state, S->state_bytes) != hipSuccess || hipMalloc(&S->d_rc, kRcStateWords * 4) != hipSuccess) {
+        session_free(S);
+        delete S;
+        return ctx->fail(LZMA_E_NOMEM, "session state");
+    }
+    ctx->session = S;
+    *out = S;
+    return LZMA_OK;
+}
+
+static int session_step(EncSession* S, uint64_t bytes) {
+    Ctx* ctx = S->ctx;
+    if (S->done) return LZMA_OK;
+    EncPass& P = S->P;
+    hipStream_t st = S->st;
+    const uint64_t stop = std::min<uint64_t>(S->n, S->in_pos + std::max<uint64_t>(bytes, 1));
+    P.slice_state = S->d_state;
+    P.slice_stop = (uint32_t)stop;
+    P.slice_resume = S->in_pos > 0 ? 1u : 0u;
+    int rc;
+    if ((rc = pass_parse(ctx, P, st))) return rc;
+    // the parser's verdict and where it stopped: the coder's flush depends on it
+    uint64_t* pw = ctx->pin.as<uint64_t>();
+    HIPCHK(hipMemcpyAsync(pw, S->d_state, SS_WORDS * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(pw + SS_WORDS / 2, P.d_status, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(pw + SS_WORDS / 2 + 1, P.d_lens, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    const uint32_t* sc = (const uint32_t*)pw;
+    const int32_t pstat = *(const int32_t*)(pw + SS_WORDS / 2);
+    if (pstat != LZMA_OK)
+        return ctx->fail(pstat, "sliced parse: consistency check tripped (%llx)", (unsigned long long)pw[SS_WORDS / 2 + 1]);
+    if (sc[SS_MAGIC] != kSliceMagic) return ctx->fail(LZMA_E_INTERNAL, "sliced parse left no state");
+    const uint64_t now_pos = sc[SS_NOW_POS];
+    const int done = sc[SS_DONE] != 0;
+    if (now_pos < S->in_pos || now_pos > S->n || (!done && now_pos < stop))
+        return ctx->fail(LZMA_E_INTERNAL, "sliced parse stopped at %llu", (unsigned long long)now_pos);
+    // the coder over this slice's records, appended at out_len
+    const uint64_t oo[2] = {S->out_len, S->out_cap};
+    memcpy(pw, oo, 16);
+    HIPCHK(hipMemcpyAsync(P.d_oofs, pw, 16, hipMemcpyHostToDevice, st));
+    RcArgs ra{};
+    ra.sliced = 1;
+    ra.flush = done ? 1u : 0u;
+    ra.init_state = S->steps > 0 ? S->d_rc : nullptr;
+    ra.end_state = S->d_rc;
+    if ((rc = pass_rc(ctx, P, P.d_rofs, P.d_rlens, P.d_order, P.d_status, P.d_oofs, P.d_lens, P.d_seg, st, &ra))) return rc;
+    HIPCHK(hipMemcpyAsync(pw + 2, P.d_lens, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(pw + 3, P.d_status, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    const int32_t cstat = *(const int32_t*)(pw + 3);
+    if (cstat != LZMA_OK) return ctx->fail(cstat, "sliced coder failed (%d)", cstat);
+    S->out_len += pw[2];
+    S->in_pos = now_pos;
+    S->done = done;
+    S->steps++;
+    return LZMA_OK;
+}
+
+static int session_save(const EncSession* S, uint8_t* blob, uint64_t cap, uint64_t* len) {
+    Ctx* ctx = S->ctx;
+    const uint64_t sb = S->done ? 0 : S->state_bytes;
+    const uint64_t need = B_WORDS * 8 + sb;
+    if (len) *len = need;
+    if (!blob) return LZMA_OK;   // size query
+    if (cap < need) return ctx->fail(LZMA_E_OVERFLOW, "blob capacity %llu < %llu", (unsigned long long)cap, (unsigned long long)need);
+    uint64_t h[B_WORDS] = {};
+    h[B_MAGIC] = kBlobMagic; h[B_VERSION] = 1;
+    h[B_DICT] = (uint32_t)S->params.dict_size; h[B_FB] = (uint32_t)S->params.fb; h[B_MF] = (uint32_t)S->params.mf;
+    h[B_LCLPPB] = (uint64_t)S->params.lc | ((uint64_t)S->params.lp << 8) | ((uint64_t)S->params.pb << 16);
+    h[B_EOS] = (uint32_t)S->params.eos; h[B_N] = S->n; h[B_IN_POS] = S->in_pos; h[B_OUT_LEN] = S->out_len;
+    h[B_DONE] = (uint64_t)S->done; h[B_STATE_BYTES] = sb;
+    uint32_t rcw[kRcStateWords] = {};
+    if (S->steps > 0) {
+        HIPCHK(hipMemcpy(rcw, S->d_rc, sizeof rcw, hipMemcpyDeviceToHost));
+    }
+    memcpy(&h[B_RC], rcw, sizeof rcw);
+    memcpy(blob, h, sizeof h);
+    if (sb) HIPCHK(hipMemcpy(blob + sizeof h, S->d_state, sb, hipMemcpyDeviceToHost));
+    return LZMA_OK;
+}
+
+static int session_restore(EncSession* S, const uint8_t* blob, uint64_t len) {
+    Ctx* ctx = S->ctx;
+    if (S->steps > 0) return ctx->fail(LZMA_E_PARAM, "restore: the session has already stepped");
+    uint64_t h[B_WORDS];
+    if (!blob || len < sizeof h) return ctx->fail(LZMA_E_PARAM, "restore: blob too short");
+    memcpy(h, blob, sizeof h);
+    const lzma_params& p = S->params;
+    if (h[B_MAGIC] != kBlobMagic || h[B_VERSION] != 1) return ctx->fail(LZMA_E_PARAM, "restore: not a session blob");
+    if (h[B_DICT] != (uint32_t)p.dict_size || h[B_FB] != (uint32_t)p.fb || h[B_MF] != (uint32_t)p.mf ||
+        h[B_LCLPPB] != ((uint64_t)p.lc | ((uint64_t)p.lp << 8) | ((uint64_t)p.pb << 16)) || h[B_EOS] != (uint32_t)p.eos ||
+        h[B_N] != S->n)
+        return ctx->fail(LZMA_E_PARAM, "restore: the blob is of other parameters or another stream length");
+    const uint64_t sb = h[B_STATE_BYTES];
+    if ((h[B_DONE] == 0 && sb != S->state_bytes) || len < sizeof h + sb || h[B_IN_POS] > S->n || h[B_OUT_LEN] > S->out_cap)
+        return ctx->fail(LZMA_E_PARAM, "restore: inconsistent blob");
+    if (h[B_IN_POS] == 0) return LZMA_OK;   // saved before the first step: nothing to restore
+    uint32_t rcw[kRcStateWords];
+    memcpy(rcw, &h[B_RC], sizeof rcw);
+    HIPCHK(hipMemcpy(S->d_rc, rcw, sizeof rcw, hipMemcpyHostToDevice));
+    if (sb) HIPCHK(hipMemcpy(S->d_state, blob + sizeof h, sb, hipMemcpyHostToDevice));
+    S->in_pos = h[B_IN_POS];
+    S->out_len = h[B_OUT_LEN];
+    S->done = (int)h[B_DONE];
+    S->steps = 1;   // the coder goes on from the blob's state
     return LZMA_OK;
 }
 
@@ -924,6 +1106,7 @@ void lzma_ctx_destroy(lzma_ctx* ctx) {
             if (o->fence == ctx) o->fence = nullptr;   // an encoder fenced on this decoder: no fence any more
     }
     hipSetDevice(ctx->device);
+    if (ctx->session) lzma_enc_session_end((lzma_enc_session*)ctx->session);   // its buffers are the context's
     ctx->resolve_timings();
     for (auto e : ctx->free_events) hipEventDestroy(e);
     if (ctx->dec_pending) hipEventSynchronize(ctx->dec_done);
@@ -1044,6 +1227,7 @@ int lzma_pack_dev(lzma_ctx* ctx, const uint8_t* d_src, const uint64_t* h_src_off
     if (ctx->dec_pending) return ctx->fail(LZMA_E_PARAM, "an asynchronous decode is in flight: lzma_dec_batch_dev_wait first");
     if (ctx->split_state || ctx->rc_pending)
         return ctx->fail(LZMA_E_PARAM, "a split encode is in flight on this context: lzma_enc_parse_dev_async / _wait first");
+    if (ctx->session) return ctx->fail(LZMA_E_PARAM, "an encode session is open on this context: lzma_enc_session_end first");
     hipSetDevice(ctx->device);
     hipStream_t st = (hipStream_t)hip_stream;
     for (int i = 0; i < nstreams; i++)
@@ -1171,6 +1355,54 @@ int lzma_match_lists(lzma_ctx* ctx, const lzma_params* p, const uint8_t* in, con
     *total_pairs = k;
     if (k > cap) return ctx->fail(LZMA_E_OVERFLOW, "%llu pairs > cap %llu", (unsigned long long)k, (unsigned long long)cap);
     return LZMA_OK;
+}
+
+int lzma_enc_session_begin(lzma_ctx* ctx, const lzma_params* p, const uint8_t* d_in, uint64_t n, uint8_t* d_out,
+                           uint64_t out_cap, void* hip_stream, lzma_enc_session** out) {
+    if (!ok_ctx(ctx) || !p || !out) return LZMA_E_PARAM;
+    *out = nullptr;
+    if (check_device(ctx)) return LZMA_E_NODEVICE;
+    hipSetDevice(ctx->device);
+    EncSession* S = nullptr;
+    int rc = session_begin(ctx, p, d_in, n, d_out, out_cap, (hipStream_t)hip_stream, &S);
+    if (rc == LZMA_OK) *out = (lzma_enc_session*)S;
+    return rc;
+}
+
+int lzma_enc_session_step(lzma_enc_session* s, uint64_t bytes, uint64_t* in_pos, uint64_t* out_len, int* done) {
+    EncSession* S = (EncSession*)s;
+    if (!ok_sess(S)) return LZMA_E_PARAM;
+    hipSetDevice(S->ctx->device);
+    int rc = session_step(S, bytes);
+    if (in_pos) *in_pos = S->in_pos;
+    if (out_len) *out_len = S->out_len;
+    if (done) *done = S->done;
+    return rc;
+}
+
+int lzma_enc_session_save(const lzma_enc_session* s, uint8_t* blob, uint64_t cap, uint64_t* len) {
+    const EncSession* S = (const EncSession*)s;
+    if (!ok_sess(S)) return LZMA_E_PARAM;
+    hipSetDevice(S->ctx->device);
+    return session_save(S, blob, cap, len);
+}
+
+int lzma_enc_session_restore(lzma_enc_session* s, const uint8_t* blob, uint64_t len) {
+    EncSession* S = (EncSession*)s;
+    if (!ok_sess(S)) return LZMA_E_PARAM;
+    hipSetDevice(S->ctx->device);
+    return session_restore(S, blob, len);
+}
+
+void lzma_enc_session_end(lzma_enc_session* s) {
+    EncSession* S = (EncSession*)s;
+    if (!ok_sess(S)) return;
+    hipSetDevice(S->ctx->device);
+    hipStreamSynchronize(S->st);
+    session_free(S);
+    if (S->ctx->session == S) S->ctx->session = nullptr;
+    S->magic = 0;
+    delete S;
 }
 
 int lzma_encode(lzma_ctx* ctx, const lzma_params* p, const uint8_t* in, uint64_t n, uint8_t* out, uint64_t out_cap,

@@ -46,6 +46,8 @@ EXPORTED_SYMBOLS = [
     "lzma_enc_batch_multi", "lzma_dec_batch_multi", "lzma_mctx_set_batch_bytes", "lzma_mctx_set_timing",
     "lzma_visible_on_error", "lzma_dec_batch_dev_async", "lzma_dec_batch_dev_wait", "lzma_ctx_set_parse_fence",
     "lzma_enc_stage_dev", "lzma_enc_parse_dev_async", "lzma_enc_parse_dev_wait",
+    "lzma_enc_session_begin", "lzma_enc_session_step", "lzma_enc_session_save", "lzma_enc_session_restore",
+    "lzma_enc_session_end",
 ]
 
 
@@ -101,6 +103,11 @@ def lib():
         L.lzma_ctx_timings.argtypes = [vp, vp, vp, vp, i32]
         L.lzma_ctx_reset_timings.argtypes = [vp]
         L.lzma_ctx_stats.argtypes = [vp, vp, vp, vp]
+        L.lzma_enc_session_begin.argtypes = [vp, P, vp, u64, vp, u64, vp, ctypes.POINTER(vp)]
+        L.lzma_enc_session_step.argtypes = [vp, u64, vp, vp, vp]
+        L.lzma_enc_session_save.argtypes = [vp, vp, u64, vp]
+        L.lzma_enc_session_restore.argtypes = [vp, vp, u64]
+        L.lzma_enc_session_end.argtypes = [vp]
         L.lzma_enc_batch_dev.argtypes = [vp, P, vp, vp, i32, vp, vp, vp, vp]
         L.lzma_enc_batch.argtypes = [vp, P, vp, vp, i32, vp, u64, vp]
         L.lzma_pack_dev.argtypes = [vp, vp, vp, vp, i32, vp, vp, vp]
@@ -414,10 +421,61 @@ class Context:
         self._async_n = 0
         return lens[:n], status[:n]
 
+    def session(self, d_in, n: int, p: Params, d_out, out_cap: int, stream_ptr: int = 0, resume: bytes = None):
+        """An EncodeSession (the sliced encode of one stream) on this context."""
+        return EncodeSession(self, d_in, n, p, d_out, out_cap, stream_ptr, resume)
+
     def set_parse_fence(self, dec_ctx: "Context | None") -> None:
         """Encode passes on this context start their parser only after dec_ctx's
         asynchronous decode in flight has finished (None clears it)."""
         self.check(lib().lzma_ctx_set_parse_fence(self.h, dec_ctx.h if dec_ctx is not None else None))
+
+
+def blob_positions(blob: bytes):
+    """(input consumed, final output bytes, done) recorded in a session blob (runtime.hip B_*)."""
+    w = np.frombuffer(blob[:11 * 8], dtype=np.uint64)
+    return int(w[8]), int(w[9]), bool(w[10])
+
+
+class EncodeSession:
+    """The sliced encode of ONE stream (lzma_enc_session_*): Encoder.Code (Encoder.java:1064-1077)
+    in bounded launches. step(nbytes) parses and codes at least nbytes more input and appends
+    the final output bytes; save() / Context.session(..., resume=blob) carry the state to another
+    process. d_in / d_out: device pointers or torch tensors, valid until close()."""
+
+    def __init__(self, ctx: "Context", d_in, n: int, p: Params, d_out, out_cap: int, stream_ptr: int = 0,
+                 resume: bytes = None):
+        self.ctx = ctx
+        self.h = ctypes.c_void_p()
+        ctx.check(lib().lzma_enc_session_begin(ctx.h, ctypes.byref(p), _dptr(d_in), n, _dptr(d_out), out_cap,
+                                               ctypes.c_void_p(stream_ptr), ctypes.byref(self.h)))
+        self.in_pos, self.out_len, self.done = 0, 0, False
+        if resume is not None:
+            buf = (ctypes.c_uint8 * len(resume)).from_buffer_copy(resume)
+            rc = lib().lzma_enc_session_restore(self.h, buf, len(resume))
+            if rc != LZMA_OK:
+                self.close()
+                ctx.check(rc)
+            self.in_pos, self.out_len, self.done = blob_positions(resume)
+
+    def step(self, nbytes: int):
+        """(input consumed, final output bytes, done) after at least nbytes more input."""
+        ip, ol, dn = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_int()
+        self.ctx.check(lib().lzma_enc_session_step(self.h, nbytes, ctypes.byref(ip), ctypes.byref(ol), ctypes.byref(dn)))
+        self.in_pos, self.out_len, self.done = int(ip.value), int(ol.value), bool(dn.value)
+        return self.in_pos, self.out_len, self.done
+
+    def save(self) -> bytes:
+        n = ctypes.c_uint64()
+        self.ctx.check(lib().lzma_enc_session_save(self.h, None, 0, ctypes.byref(n)))
+        buf = (ctypes.c_uint8 * n.value)()
+        self.ctx.check(lib().lzma_enc_session_save(self.h, buf, n.value, ctypes.byref(n)))
+        return bytes(buf[:n.value])
+
+    def close(self):
+        if self.h:
+            lib().lzma_enc_session_end(self.h)
+            self.h = ctypes.c_void_p()
 
 
 class MultiContext:

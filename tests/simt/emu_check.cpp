@@ -12,7 +12,7 @@
 #include "../../include/lzma_mi355x.h"
 #include "../../oracle/lzma_oracle.h"
 
-namespace lzg { alignas(16) uint8_t smem[160 * 1024]; }
+namespace lzg { alignas(16) uint8_t smem[160 * 1024]; namespace sliced { alignas(16) uint8_t smem[160 * 1024]; } }
 
 static std::vector<uint8_t> make_input(int kind, size_t n, unsigned seed) {
     std::vector<uint8_t> v(n);

@@ -366,3 +366,77 @@ def test_split_failure_after_consumption_drops_staged(where):
     assert "error" not in r, r.get("error")
     assert r == {"failed": True, "code_not_param": True, "wrapper_dropped": True, "then_refused": True,
                  "after_equal": True}, r
+
+
+def _session_worker(q, cases):
+    import lzma_amd
+    import oracle_ffi as orc
+    lzma_amd.LIB_PATH = SIMT_LIB   # "device" pointers are host pointers in the emulation
+    try:
+        res = []
+        for kind, n, dict_log, fb, lc, lp, pb, eos, slice_bytes, hop in cases:
+            data = (lzma_amd.bench_generate(n) if kind == "bench" else lzma_amd.text_generate(n, 3)).tobytes()
+            p = lzma_amd.make_params(dict_size=1 << dict_log, fb=fb, mf=1, lc=lc, lp=lp, pb=pb, eos=eos)
+            ref = orc.encode(data, orc.params(p.dict_size, p.fb, p.mf, p.lc, p.lp, p.pb, p.eos))
+            src = np.frombuffer(data + b"\0" * 16, dtype=np.uint8).copy()
+            cap = lzma_amd.enc_bound(n)
+            out = np.zeros(cap + 1, dtype=np.uint8)
+            ctx = lzma_amd.Context(0)
+            s = ctx.session(src.ctypes.data, n, p, out.ctypes.data, cap)
+            steps, progress = 0, []
+            while not s.done:
+                if hop and steps == hop:   # checkpoint, a new context and session, restore
+                    blob = s.save()
+                    s.close()
+                    ctx.close()
+                    kept = out[:s.out_len].copy()
+                    out[:] = 0xAB   # the new session must only write after the kept prefix
+                    out[:kept.size] = kept
+                    ctx = lzma_amd.Context(0)
+                    s = ctx.session(src.ctypes.data, n, p, out.ctypes.data, cap, resume=blob)
+                progress.append(s.step(slice_bytes)[:2])
+                steps += 1
+            # while open, the context's other entry points refuse
+            try:
+                ctx.encode_batch([data[:10]], p)
+                refused = False
+            except lzma_amd.LzmaError as e:
+                refused = e.code == lzma_amd.LZMA_E_PARAM
+            got = out[:s.out_len].tobytes()
+            s.close()
+            ctx.close()
+            mono = all(a[0] <= b[0] and a[1] <= b[1] for a, b in zip(progress, progress[1:]))
+            res.append(dict(equal=got == ref, steps=steps, refused=refused, monotone=mono, n=n))
+        q.put(res)
+    except BaseException as e:   # reported to the parent
+        import traceback
+        q.put(dict(error=traceback.format_exc()))
+
+
+@pytest.mark.timeout(900)
+def test_session_sliced_encode_emulated():
+    """The sliced encode (lzma_enc_session_*): one stream encoded in launches that stop at
+    CodeOneBlock boundaries, the range coder carrying its state from slice to slice, and a
+    checkpoint restored on a fresh context, gives exactly Encoder.Code's bytes (the oracle),
+    over the bench and text data, the level-5 kernel (SPEC 1), other fb / lc / lp / pb, the
+    end marker, tiny slices and one slice for the whole stream."""
+    subprocess.check_call(["make", "-s", "-j", "8", "-C", SIMT, "so"])
+    cases = [
+        ("bench", 60000, 20, 32, 3, 0, 2, 0, 7000, 0),     # SPEC 1 (the bench parameters), 8+ slices
+        ("bench", 60000, 20, 32, 3, 0, 2, 0, 5000, 3),     # ... with a checkpoint / restore after 3 steps
+        ("text", 50000, 16, 64, 0, 2, 1, 1, 9000, 2),      # fb > 32, lc0 lp2 pb1, end marker, restore
+        ("text", 30000, 20, 5, 8, 0, 4, 0, 1, 0),          # slices of 1 byte (one block each), lc8, pb4
+        ("bench", 40000, 20, 273, 3, 0, 2, 0, 1 << 30, 0),  # one slice: the whole stream
+        ("bench", 0, 20, 32, 3, 0, 2, 1, 1000, 0),          # empty stream, end marker
+        ("bench", 1500000, 22, 32, 3, 0, 2, 0, 600000, 1),  # slices of > 2^20 records: 16 coder segments each
+    ]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    pr = ctx.Process(target=_session_worker, args=(q, cases))
+    pr.start()
+    r = q.get(timeout=800)
+    pr.join(timeout=60)
+    assert not isinstance(r, dict), r.get("error")
+    for c, x in zip(cases, r):
+        assert x["equal"] and x["refused"] and x["monotone"], (c, x)
+    assert r[0]["steps"] >= 8 and r[3]["steps"] > 100 and r[4]["steps"] == 1
