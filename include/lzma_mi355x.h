@@ -184,6 +184,13 @@ int lzma_enc_session_step(lzma_enc_session *s, uint64_t bytes, uint64_t *in_pos,
 int lzma_enc_session_save(const lzma_enc_session *s, uint8_t *blob, uint64_t cap, uint64_t *len);
 int lzma_enc_session_restore(lzma_enc_session *s, const uint8_t *blob, uint64_t len);
 void lzma_enc_session_end(lzma_enc_session *s);
+/* Host-buffer form (the JNI drop-in's Encoder.Code with an ICodeProgress): the input is
+ * copied to the context's device staging; after each step, lzma_enc_session_output copies
+ * final output bytes [from, from + len), from + len <= *out_len, to the host, so the caller
+ * can write them to its OutputStream and call SetProgress(in_pos, out_len) slice by slice. */
+int lzma_enc_session_begin_host(lzma_ctx *ctx, const lzma_params *p, const uint8_t *in, uint64_t n,
+                                lzma_enc_session **out);
+int lzma_enc_session_output(const lzma_enc_session *s, uint64_t from, uint8_t *dst, uint64_t len);
 
 /* ---- decode -------------------------------------------------------------
  * props: the 5 property bytes (Decoder.SetDecoderProperties).

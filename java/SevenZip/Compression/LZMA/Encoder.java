@@ -79,13 +79,45 @@ public class Encoder {
         }
     }
 
+    /** Input bytes per device launch of a long stream's sliced encode (lzma_enc_session_*). */
+    static final int kSliceBytes = 16 << 20;
+
     /** Encoder.Code (Encoder.java:1064-1077): reads inStream to EOF, writes the raw stream;
-     *  inSize/outSize are ignored as in the reference (Encoder.java:1046); progress is
-     *  reported once, at the end (no output bit depends on it). */
+     *  inSize/outSize are ignored as in the reference (Encoder.java:1046). A stream longer than
+     *  one slice is encoded slice by slice (the same bytes): each slice's final output goes to
+     *  outStream as it is produced and progress is reported after every slice, as the reference
+     *  writes while it codes and reports per block (Encoder.java:1069-1073); a shorter one in one
+     *  call, with progress reported once at the end (no output bit depends on it). */
     public void Code(InputStream inStream, OutputStream outStream, long inSize, long outSize,
                      ICodeProgress progress) throws IOException {
         int[] n = new int[1];
         byte[] src = Native.readAll(inStream, n);
+        if (n[0] > kSliceBytes) {
+            long h = Native.sessionBegin(src, n[0], _dictionarySize, _numFastBytes, _matchFinderType,
+                    _numLiteralContextBits, _numLiteralPosStateBits, _posStateBits, _writeEndMark);
+            try {
+                long[] pos = new long[2];
+                long written = 0;
+                byte[] buf = new byte[1 << 20];
+                boolean done;
+                do {
+                    done = Native.sessionStep(h, kSliceBytes, pos);
+                    while (written < pos[1]) {
+                        int k = (int) Math.min(buf.length, pos[1] - written);
+                        Native.sessionOutput(h, written, buf, k);
+                        outStream.write(buf, 0, k);
+                        written += k;
+                    }
+                    if (progress != null) {
+                        progress.SetProgress(pos[0], pos[1]);
+                    }
+                } while (!done);
+            } finally {
+                Native.sessionEnd(h);
+            }
+            outStream.flush();
+            return;
+        }
         byte[] enc = Native.encode(src, n[0], _dictionarySize, _numFastBytes, _matchFinderType,
                 _numLiteralContextBits, _numLiteralPosStateBits, _posStateBits, _writeEndMark);
         outStream.write(enc);

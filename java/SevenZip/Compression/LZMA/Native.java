@@ -35,6 +35,18 @@ final class Native {
     static native long[] encodeBatch(byte[] in, long[] offs, byte[] out,
                                      int dict, int fb, int mf, int lc, int lp, int pb, boolean eos);
 
+    /** The sliced encode of in[0..len) (lzma_enc_session_*): a handle for the calls below. */
+    static native long sessionBegin(byte[] in, int len, int dict, int fb, int mf, int lc, int lp, int pb, boolean eos);
+
+    /** At least bytes more input parsed and coded; pos[0] = input consumed, pos[1] = output bytes
+     *  final so far; true once the stream is flushed. */
+    static native boolean sessionStep(long h, long bytes, long[] pos);
+
+    /** Final output bytes [from, from + len) into dst[0..len). */
+    static native void sessionOutput(long h, long from, byte[] dst, int len);
+
+    static native void sessionEnd(long h);
+
     /** The whole of in: Encoder.Code reads its input to EOF (InWindow.java:47-56). */
     static byte[] readAll(InputStream in, int[] len) throws IOException {
         byte[] buf = new byte[1 << 16];

@@ -26,6 +26,7 @@
 
 static lzma_mctx *g_m;
 static lzma_ctx *g_ctx;
+static int g_dev0;   /* the first device of the mask (init) */
 static pthread_mutex_t g_lock = PTHREAD_MUTEX_INITIALIZER;
 
 static void throw_io(JNIEnv *env, const char *msg) {
@@ -43,6 +44,7 @@ JNIEXPORT jboolean JNICALL Java_SevenZip_Compression_LZMA_Native_init(JNIEnv *en
         int first = 0;
         while (!(m >> first & 1u)) first++;
         ok = lzma_ctx_create(first, &g_ctx) == LZMA_OK;
+        g_dev0 = first;
         if (!ok) {   /* no half-initialised state: the next init starts over */
             lzma_mctx_destroy(g_m);
             g_m = NULL;
@@ -171,4 +173,79 @@ JNIEXPORT jlongArray JNICALL Java_SevenZip_Compression_LZMA_Native_encodeBatch(
     if (r) (*env)->SetLongArrayRegion(env, r, 0, n + 1, (const jlong *)oo);
     free(oo);
     return r;
+}
+
+/* The sliced encode (lzma_enc_session_*) for Encoder.Code on a long stream: the drop-in's
+ * Code loop steps it a slice at a time, writes each slice's final bytes to its OutputStream
+ * and calls ICodeProgress.SetProgress between slices (Encoder.java:1069-1073 reports per
+ * block). A session owns a context of its own (an open session refuses the context's other
+ * calls), so other threads' Code calls keep the shared one. The handle is a jlong. */
+typedef struct {
+    lzma_ctx *ctx;
+    lzma_enc_session *s;
+} jsession;
+
+/* static native long sessionBegin(byte[] in, int len, int dict, int fb, int mf, int lc, int lp, int pb, boolean eos) */
+JNIEXPORT jlong JNICALL Java_SevenZip_Compression_LZMA_Native_sessionBegin(
+        JNIEnv *env, jclass cls, jbyteArray in, jint n, jint dict, jint fb, jint mf,
+        jint lc, jint lp, jint pb, jboolean eos) {
+    (void)cls;
+    lzma_params p = {dict, fb, mf, lc, lp, pb, eos ? 1 : 0};
+    jsession *js = (jsession *)calloc(1, sizeof *js);
+    if (!js) { throw_io(env, "out of memory"); return 0; }
+    pthread_mutex_lock(&g_lock);
+    const int dev = g_dev0;
+    pthread_mutex_unlock(&g_lock);
+    if (lzma_ctx_create(dev, &js->ctx) != LZMA_OK) { free(js); throw_io(env, "no MI355X device for the session"); return 0; }
+    jbyte *src = (*env)->GetPrimitiveArrayCritical(env, in, NULL);
+    if (!src) { lzma_ctx_destroy(js->ctx); free(js); return 0; }
+    int rc = lzma_enc_session_begin_host(js->ctx, &p, (const uint8_t *)src, (uint64_t)n, &js->s);
+    (*env)->ReleasePrimitiveArrayCritical(env, in, src, JNI_ABORT);
+    if (rc != LZMA_OK) {
+        throw_io(env, lzma_last_error(js->ctx));
+        lzma_ctx_destroy(js->ctx);
+        free(js);
+        return 0;
+    }
+    return (jlong)(intptr_t)js;
+}
+
+/* static native boolean sessionStep(long h, long bytes, long[] pos): pos[0] = input consumed,
+ * pos[1] = output bytes final so far; returns true once the stream is flushed */
+JNIEXPORT jboolean JNICALL Java_SevenZip_Compression_LZMA_Native_sessionStep(
+        JNIEnv *env, jclass cls, jlong h, jlong bytes, jlongArray pos) {
+    (void)cls;
+    jsession *js = (jsession *)(intptr_t)h;
+    if (!js) { throw_io(env, "closed session"); return JNI_FALSE; }
+    uint64_t ip = 0, ol = 0;
+    int done = 0;
+    int rc = lzma_enc_session_step(js->s, bytes > 0 ? (uint64_t)bytes : 1u, &ip, &ol, &done);
+    if (rc != LZMA_OK) { throw_io(env, lzma_last_error(js->ctx)); return JNI_FALSE; }
+    jlong v[2] = {(jlong)ip, (jlong)ol};
+    (*env)->SetLongArrayRegion(env, pos, 0, 2, v);
+    return done ? JNI_TRUE : JNI_FALSE;
+}
+
+/* static native void sessionOutput(long h, long from, byte[] dst, int len): final output bytes */
+JNIEXPORT void JNICALL Java_SevenZip_Compression_LZMA_Native_sessionOutput(
+        JNIEnv *env, jclass cls, jlong h, jlong from, jbyteArray dst, jint len) {
+    (void)cls;
+    jsession *js = (jsession *)(intptr_t)h;
+    if (!js) { throw_io(env, "closed session"); return; }
+    if (len <= 0) return;
+    jbyte *d = (*env)->GetPrimitiveArrayCritical(env, dst, NULL);
+    if (!d) return;
+    int rc = lzma_enc_session_output(js->s, (uint64_t)from, (uint8_t *)d, (uint64_t)len);
+    (*env)->ReleasePrimitiveArrayCritical(env, dst, d, 0);
+    if (rc != LZMA_OK) throw_io(env, lzma_last_error(js->ctx));
+}
+
+/* static native void sessionEnd(long h) */
+JNIEXPORT void JNICALL Java_SevenZip_Compression_LZMA_Native_sessionEnd(JNIEnv *env, jclass cls, jlong h) {
+    (void)env; (void)cls;
+    jsession *js = (jsession *)(intptr_t)h;
+    if (!js) return;
+    lzma_enc_session_end(js->s);
+    lzma_ctx_destroy(js->ctx);
+    free(js);
 }

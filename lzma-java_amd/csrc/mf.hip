@@ -397,6 +397,8 @@ __global__ void __launch_bounds__(256) mf_long_scatter_kernel(const uint32_t* __
 
 #ifdef LZG_WALK_WAVES   // experiment: a VGPR budget for more waves per SIMD (memory-level parallelism)
 #define LZG_WALK_ATTR __attribute__((amdgpu_waves_per_eu(LZG_WALK_WAVES, LZG_WALK_WAVES)))
+#elif defined(LZG_WALK_VGPRS)   // experiment: an explicit VGPR cap
+#define LZG_WALK_ATTR __attribute__((amdgpu_num_vgpr(LZG_WALK_VGPRS)))
 #else
 #define LZG_WALK_ATTR
 #endif

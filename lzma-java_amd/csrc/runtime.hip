@@ -1369,6 +1369,36 @@ int lzma_enc_session_begin(lzma_ctx* ctx, const lzma_params* p, const uint8_t* d
     return rc;
 }
 
+int lzma_enc_session_begin_host(lzma_ctx* ctx, const lzma_params* p, const uint8_t* in, uint64_t n,
+                                lzma_enc_session** out) {
+    if (!ok_ctx(ctx) || !p || !out || (n && !in)) return LZMA_E_PARAM;
+    *out = nullptr;
+    if (check_device(ctx)) return LZMA_E_NODEVICE;
+    hipSetDevice(ctx->device);
+    if (ctx->dec_pending || ctx->split_state || ctx->rc_pending || ctx->session)
+        return ctx->fail(LZMA_E_PARAM, "the context is busy (a decode, split encode or session in flight)");
+    const uint64_t cap = lzma_enc_bound(n);
+    // the context's staging buffers (grown, never shrunk): no allocation per call once sized
+    if (!ctx->io_in.ensure(n + 1) || !ctx->io_out.ensure(cap + 1)) return ctx->fail(LZMA_E_NOMEM, "device staging buffers");
+    if (n) HIPCHK(hipMemcpy(ctx->io_in.as<uint8_t>(), in, n, hipMemcpyHostToDevice));
+    EncSession* S = nullptr;
+    int rc = session_begin(ctx, p, ctx->io_in.as<uint8_t>(), n, ctx->io_out.as<uint8_t>(), cap, nullptr, &S);
+    if (rc == LZMA_OK) *out = (lzma_enc_session*)S;
+    return rc;
+}
+
+int lzma_enc_session_output(const lzma_enc_session* s, uint64_t from, uint8_t* dst, uint64_t len) {
+    const EncSession* S = (const EncSession*)s;
+    if (!ok_sess(S) || (len && !dst)) return LZMA_E_PARAM;
+    Ctx* ctx = S->ctx;
+    if (from > S->out_len || len > S->out_len - from)
+        return ctx->fail(LZMA_E_PARAM, "output [%llu, +%llu) is not final yet (%llu bytes are)", (unsigned long long)from,
+                         (unsigned long long)len, (unsigned long long)S->out_len);
+    hipSetDevice(ctx->device);
+    if (len) HIPCHK(hipMemcpy(dst, S->P.d_out + from, len, hipMemcpyDeviceToHost));
+    return LZMA_OK;
+}
+
 int lzma_enc_session_step(lzma_enc_session* s, uint64_t bytes, uint64_t* in_pos, uint64_t* out_len, int* done) {
     EncSession* S = (EncSession*)s;
     if (!ok_sess(S)) return LZMA_E_PARAM;

@@ -47,7 +47,7 @@ EXPORTED_SYMBOLS = [
     "lzma_visible_on_error", "lzma_dec_batch_dev_async", "lzma_dec_batch_dev_wait", "lzma_ctx_set_parse_fence",
     "lzma_enc_stage_dev", "lzma_enc_parse_dev_async", "lzma_enc_parse_dev_wait",
     "lzma_enc_session_begin", "lzma_enc_session_step", "lzma_enc_session_save", "lzma_enc_session_restore",
-    "lzma_enc_session_end",
+    "lzma_enc_session_end", "lzma_enc_session_begin_host", "lzma_enc_session_output",
 ]
 
 
@@ -108,6 +108,8 @@ def lib():
         L.lzma_enc_session_save.argtypes = [vp, vp, u64, vp]
         L.lzma_enc_session_restore.argtypes = [vp, vp, u64]
         L.lzma_enc_session_end.argtypes = [vp]
+        L.lzma_enc_session_begin_host.argtypes = [vp, P, vp, u64, ctypes.POINTER(vp)]
+        L.lzma_enc_session_output.argtypes = [vp, u64, vp, u64]
         L.lzma_enc_batch_dev.argtypes = [vp, P, vp, vp, i32, vp, vp, vp, vp]
         L.lzma_enc_batch.argtypes = [vp, P, vp, vp, i32, vp, u64, vp]
         L.lzma_pack_dev.argtypes = [vp, vp, vp, vp, i32, vp, vp, vp]
@@ -425,6 +427,10 @@ class Context:
         """An EncodeSession (the sliced encode of one stream) on this context."""
         return EncodeSession(self, d_in, n, p, d_out, out_cap, stream_ptr, resume)
 
+    def session_host(self, data: bytes, p: Params):
+        """An EncodeSession over host bytes (lzma_enc_session_begin_host); read its output with .output()."""
+        return EncodeSession(self, None, len(data), p, None, 0, host=data)
+
     def set_parse_fence(self, dec_ctx: "Context | None") -> None:
         """Encode passes on this context start their parser only after dec_ctx's
         asynchronous decode in flight has finished (None clears it)."""
@@ -444,11 +450,16 @@ class EncodeSession:
     process. d_in / d_out: device pointers or torch tensors, valid until close()."""
 
     def __init__(self, ctx: "Context", d_in, n: int, p: Params, d_out, out_cap: int, stream_ptr: int = 0,
-                 resume: bytes = None):
+                 resume: bytes = None, host: bytes = None):
         self.ctx = ctx
         self.h = ctypes.c_void_p()
-        ctx.check(lib().lzma_enc_session_begin(ctx.h, ctypes.byref(p), _dptr(d_in), n, _dptr(d_out), out_cap,
-                                               ctypes.c_void_p(stream_ptr), ctypes.byref(self.h)))
+        if host is not None:   # lzma_enc_session_begin_host: the input from host memory
+            self._src = np.frombuffer(host, dtype=np.uint8) if not isinstance(host, np.ndarray) else host
+            ctx.check(lib().lzma_enc_session_begin_host(ctx.h, ctypes.byref(p), self._src.ctypes.data, self._src.size,
+                                                        ctypes.byref(self.h)))
+        else:
+            ctx.check(lib().lzma_enc_session_begin(ctx.h, ctypes.byref(p), _dptr(d_in), n, _dptr(d_out), out_cap,
+                                                   ctypes.c_void_p(stream_ptr), ctypes.byref(self.h)))
         self.in_pos, self.out_len, self.done = 0, 0, False
         if resume is not None:
             buf = (ctypes.c_uint8 * len(resume)).from_buffer_copy(resume)
@@ -464,6 +475,12 @@ class EncodeSession:
         self.ctx.check(lib().lzma_enc_session_step(self.h, nbytes, ctypes.byref(ip), ctypes.byref(ol), ctypes.byref(dn)))
         self.in_pos, self.out_len, self.done = int(ip.value), int(ol.value), bool(dn.value)
         return self.in_pos, self.out_len, self.done
+
+    def output(self, start: int, length: int) -> bytes:
+        """lzma_enc_session_output: final output bytes [start, start + length) to the host."""
+        buf = np.zeros(max(length, 1), dtype=np.uint8)
+        self.ctx.check(lib().lzma_enc_session_output(self.h, start, buf.ctypes.data, length))
+        return buf[:length].tobytes()
 
     def save(self) -> bytes:
         n = ctypes.c_uint64()
@@ -636,9 +653,28 @@ class Encoder:
     def WriteCoderProperties(self, outStream):   # :1079-1085
         outStream.write(write_props(self._p))
 
+    # input bytes per device launch of a long stream's sliced encode (lzma_enc_session_*)
+    SLICE_BYTES = 16 << 20
+
     def Code(self, inStream, outStream, inSize: int = -1, outSize: int = -1, progress=None):   # :1064-1077
         data = _read_all(inStream)
         ctx = self._ctx or default_context()
+        if len(data) > self.SLICE_BYTES:
+            # slice by slice (the same bytes): each slice's final output is written as it is
+            # produced and progress reported per slice, as the reference writes while it codes
+            # and reports per block (Encoder.java:1069-1073)
+            s = ctx.session_host(data, self._p)
+            try:
+                written = 0
+                while not s.done:
+                    in_pos, out_len, _ = s.step(self.SLICE_BYTES)
+                    outStream.write(s.output(written, out_len - written))
+                    written = out_len
+                    if progress is not None:
+                        progress.SetProgress(in_pos, out_len)
+            finally:
+                s.close()
+            return
         out = ctx.encode_batch([data], self._p)[0]
         outStream.write(out)
         if progress is not None:   # ICodeProgress.SetProgress, once at the end (no output bits depend on it)

@@ -440,3 +440,79 @@ def test_session_sliced_encode_emulated():
     for c, x in zip(cases, r):
         assert x["equal"] and x["refused"] and x["monotone"], (c, x)
     assert r[0]["steps"] >= 8 and r[3]["steps"] > 100 and r[4]["steps"] == 1
+
+
+def _code_worker(q):
+    import io
+    import lzma_amd
+    import oracle_ffi as orc
+    lzma_amd.LIB_PATH = SIMT_LIB   # "device" pointers are host pointers in the emulation
+    try:
+        data = lzma_amd.bench_generate(150000).tobytes()
+        enc = lzma_amd.Encoder(lzma_amd.Context(0))
+        enc.SetDictionarySize(1 << 20)
+        enc.SetNumFastBytes(32)
+        ref = orc.encode(data, orc.params(1 << 20, 32, 1, 3, 0, 2, 0))
+
+        class Prog:
+            calls = []
+
+            def SetProgress(self, i, o):
+                self.calls.append((i, o))
+
+        class Sink(io.BytesIO):
+            writes = 0
+
+            def write(self, b):
+                Sink.writes += 1
+                return super().write(b)
+
+        r = {}
+        lzma_amd.Encoder.SLICE_BYTES = 20000   # the sliced path for this 150 kB stream
+        out, pg = Sink(), Prog()
+        enc.Code(io.BytesIO(data), out, -1, -1, pg)
+        r["sliced_equal"] = out.getvalue() == ref
+        r["progress_calls"] = len(pg.calls)
+        r["progress_last"] = pg.calls[-1] == (len(data), len(ref))
+        r["progress_monotone"] = all(a <= b for a, b in zip(pg.calls, pg.calls[1:]))
+        r["streamed_writes"] = Sink.writes
+        lzma_amd.Encoder.SLICE_BYTES = 16 << 20   # one call: progress once
+        out2, pg2 = io.BytesIO(), Prog()
+        Prog.calls = []
+        enc.Code(io.BytesIO(data), out2, -1, -1, pg2)
+        r["whole_equal"] = out2.getvalue() == ref
+        r["whole_progress_calls"] = len(pg2.calls)
+        # lzma_enc_session_output refuses bytes that are not final yet
+        ctx = lzma_amd.Context(0)
+        s = ctx.session_host(data, enc.params())
+        s.step(30000)
+        try:
+            s.output(0, s.out_len + 1)
+            r["refuses_unfinal"] = False
+        except lzma_amd.LzmaError as e:
+            r["refuses_unfinal"] = e.code == lzma_amd.LZMA_E_PARAM
+        s.close()
+        ctx.close()
+        q.put(r)
+    except BaseException:
+        import traceback
+        q.put(dict(error=traceback.format_exc()))
+
+
+@pytest.mark.timeout(600)
+def test_encoder_code_sliced_streams_output_and_progress_emulated():
+    """The Java-style Encoder.Code on a stream longer than a slice (the drop-in's path,
+    java/SevenZip/Compression/LZMA/Encoder.java): the host-buffer session writes each
+    slice's final bytes as they are produced and reports progress per slice (the reference
+    reports per block, Encoder.java:1069-1073); the bytes equal Encoder.Code's (the oracle)."""
+    subprocess.check_call(["make", "-s", "-j", "8", "-C", SIMT, "so"])
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    pr = ctx.Process(target=_code_worker, args=(q,))
+    pr.start()
+    r = q.get(timeout=500)
+    pr.join(timeout=60)
+    assert "error" not in r, r.get("error")
+    assert r["sliced_equal"] and r["whole_equal"] and r["progress_last"] and r["progress_monotone"], r
+    assert r["progress_calls"] >= 7 and r["streamed_writes"] >= 7 and r["whole_progress_calls"] == 1, r
+    assert r["refuses_unfinal"], r

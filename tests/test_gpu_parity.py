@@ -709,3 +709,47 @@ def test_gpu_config4_shape_one_stream_longer_than_dict(ctx, heartbeat):
                                                                                 len(out) / n), flush=True)
     assert len(out) == len(ref)
     assert out == ref
+
+
+def test_gpu_session_sliced_encode_with_checkpoint(heartbeat):
+    """The sliced encode (lzma_enc_session_*, enc_slice.hip) on the GPU: one 20 MiB BENCH
+    stream at dict 2^26 L5 (64-bit pairs, the level-5 kernel) in 4 MiB slices, checkpointed
+    after two slices and finished by a fresh context restored from the blob, byte-equal to the
+    oracle's Encoder.Code; then a small stream with other parameters (fb 64, lc0 lp2 pb1, end
+    marker) in 64 KiB slices. Config 4's 1 GiB stream runs through this path across several
+    processes (tools/r06/config4_sliced.py)."""
+    import concurrent.futures as cf
+    import torch
+    dev = torch.device("cuda", 0)
+    st = torch.cuda.current_stream(dev).cuda_stream
+    cases = [(lzma_amd.bench_generate(20 << 20), lzma_amd.make_params(dict_size=1 << 26, fb=32, mf=1), 4 << 20, 2),
+             (lzma_amd.text_generate(1 << 20, 5), lzma_amd.make_params(dict_size=1 << 20, fb=64, mf=1, lc=0, lp=2, pb=1,
+                                                                        eos=1), 64 << 10, 5)]
+    for data, p, slice_bytes, hop in cases:
+        n = data.size
+        with cf.ThreadPoolExecutor(1) as ex:
+            fut = ex.submit(lambda: orc.EncoderSession(_oparams(p)).encode(data.tobytes()))
+            d_in = torch.from_numpy(data).to(dev)
+            cap = lzma_amd.enc_bound(n)
+            d_out = torch.zeros(cap + 1, dtype=torch.uint8, device=dev)
+            c = lzma_amd.Context(0)
+            s = c.session(d_in, n, p, d_out, cap, st)
+            steps = 0
+            while not s.done:
+                if steps == hop:
+                    blob = s.save()
+                    kept = d_out[:s.out_len].clone()
+                    s.close()
+                    c.close()
+                    d_out.fill_(0xAB)
+                    d_out[:kept.numel()] = kept
+                    c = lzma_amd.Context(0)
+                    s = c.session(d_in, n, p, d_out, cap, st, resume=blob)
+                s.step(slice_bytes)
+                steps += 1
+            got = d_out[:s.out_len].cpu().numpy().tobytes()
+            s.close()
+            c.close()
+            ref = fut.result()
+        assert steps > hop
+        assert len(got) == len(ref) and got == ref

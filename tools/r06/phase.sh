@@ -1,8 +1,9 @@
 #!/bin/bash
-# Round 5: per-phase cycle profile of the parse (LZG_PROF build, `make -C lzma-java_amd prof`):
+# Build first, here on the CPU: make -C lzma-java_amd prof (build/prof/liblzma_mi355x.so travels with the tree).
+# Round 6 (from round 5): per-phase cycle profile of the parse (LZG_PROF build, `make -C lzma-java_amd prof`):
 # one 4 MiB stream, then 256 and 4096 streams of 256 KiB (BENCH data, dict 2^26, L5)
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-O=$R/gpurun_out/r05/${TAG:-phase}
+O=$R/gpurun_out/r06/${TAG:-phase}
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
 fail() { echo "$1 failed rc=$2"; exit $2; }

@@ -1,13 +1,13 @@
 #!/bin/bash
-# Round 5 profile of one bench step (GPU box, via gpurun), DATA=bench (default) or text:
+# Round 6 profile of one bench step (GPU box, via gpurun), DATA=bench (default) or text:
 #   ${P}kernel_stats.csv  rocprofv3 --kernel-trace --stats of one bench step
 #   ${P}traffic.json      separate FETCH_SIZE / WRITE_SIZE passes (per launch)
 #   ${P}issue.json        SQ_INSTS_* issue counters (one pass)
-# with P = "" (bench) or "text_" under gpurun_out/r05/prof/. Every GPU step has its own time
+# with P = "" (bench) or "text_" under gpurun_out/r06/prof/. Every GPU step has its own time
 # limit; the first failure ends the script.
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 DATA=${DATA:-bench}
-O=$R/gpurun_out/r05/prof
+O=$R/gpurun_out/r06/prof
 mkdir -p $O
 P=""; DL=26; [ "$DATA" = text ] && { P="text_"; DL=28; }
 cd /tmp && export TMPDIR=/tmp

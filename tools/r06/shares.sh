@@ -1,9 +1,9 @@
 #!/bin/bash
-# Round 5 strong-scaling projection: rank 0's share of the 1 GiB bench buffer dealt over G GPUs,
+# Round 6 (from round 5) strong-scaling projection: rank 0's share of the 1 GiB bench buffer dealt over G GPUs,
 # timed on one GPU with the default pipelined schedule (bench.py --project-share G; the parse
-# fence is skipped at <= 8 streams per CU). One JSON line per G in gpurun_out/r05/shares.jsonl.
+# fence is skipped at <= 8 streams per CU). One JSON line per G in gpurun_out/r06/shares.jsonl.
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-O=$R/gpurun_out/r05
+O=$R/gpurun_out/r06
 mkdir -p $O
 for G in ${GS:-2 4 8}; do
   timeout -k 10 300 python3 $R/bench.py --project-share $G --pipeline ${PIPE:-split} --steps ${STEPS:-3} --warmup 1 --cpu-sample 0 --single-stream 0 --parity-streams 32 >> $O/${SH:-shares}.jsonl 2>> $O/${SH:-shares}.err || { echo "share $G failed rc=$?"; exit 1; }
