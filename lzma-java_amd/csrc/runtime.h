@@ -362,6 +362,9 @@ int mf_count_enqueue(Ctx* ctx, const MfBuffers& w, int nstreams, hipStream_t st,
 int mf_walk_launch(Ctx* ctx, const Derived& d, const uint8_t* in, const uint64_t* d_offs, int nstreams, uint64_t total,
                    bool wide_pairs, MfBuffers& w, hipStream_t st, int slot);
 int mf_walk_result(Ctx* ctx, int slot);
+// sort.hip: stable per-stream radix sort by the low end_bit key bits; the `hist` words it
+// needs for n items in nstreams segments
+size_t sort_hist_words(uint64_t n, int nstreams);
 // sort.hip: stable per-stream radix sort by the low end_bit key bits
 int seg_radix_sort(Ctx* ctx, bool key64, const void* kin, const uint32_t* vin, void* kout, uint32_t* vout,
                    uint64_t* tmp_a, uint64_t* tmp_b, uint32_t* hist, uint64_t n, const uint64_t* d_offs, int nstreams,

@@ -199,7 +199,7 @@ static int pass_carve(Ctx* ctx, EncPass& P) {
         w.chain_idx = c.take<uint32_t>(T); w.chain_order = c.take<uint32_t>(T);
         w.cls = c.take<uint32_t>(96);
         w.son = c.take<uint64_t>(4 * T);   // mf.hip WNode: 32 bytes per position
-        w.hist = c.take<uint32_t>((size_t)ns * 1024);
+        w.hist = c.take<uint32_t>(sort_hist_words(T, ns));
         w.seg_end = c.take<uint64_t>((size_t)ns + 1);
         w.chain_offs = c.take<uint64_t>((size_t)ns + 1);
     };

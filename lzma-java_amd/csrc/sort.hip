@@ -40,6 +40,13 @@ enum { SK_PACKED = 0, SK_KEY64 = 1, SK_KEY32 = 2 };
 constexpr size_t kHistLds = (size_t)kSortWaves * kMaxPasses * 256 * 4;
 constexpr size_t kPassLds = (size_t)kSortTile * 8 + 4 * 256 * 4 + (size_t)kSortWaves * 256 * 4;
 
+// One long segment (a single stream: config 4's 1 GiB stream, the JNI single-stream path)
+// would leave all but one workgroup idle, so it is cut into chunks of kChunk items, one
+// workgroup each: per pass, a histogram per chunk of that pass's input (chunk_hist_kernel),
+// a scan over the chunks giving each chunk's bucket bases (chunk_scan_kernel), then the same
+// tile pass per chunk. Stable: the chunks are in position order and each is ranked in order.
+constexpr uint64_t kChunk = 1u << 16;
+
 struct SortPass {
     const void* kin;          // SK_KEY64 / SK_KEY32 keys, or packed items (SK_PACKED)
     const uint32_t* vin;      // positions (first pass only)
@@ -50,6 +57,7 @@ struct SortPass {
     const uint64_t* dofs;     // where the last pass writes segment s (compaction), or null: offs[s]
     const uint32_t* hist;     // [nstreams][kMaxPasses][256]
     uint32_t pass, shift, bits, end_bit;
+    const uint32_t* cbase;    // chunked (one segment): bucket bases per chunk [nchunks][256], else null
 };
 
 __device__ __forceinline__ uint32_t lanemask_count(uint64_t m) {   // set bits of m below this lane
@@ -103,6 +111,52 @@ __global__ void __launch_bounds__(kSortThreads) seg_hist_kernel(SortPass a, uint
     }
 }
 
+// the chunked form's histograms: chunk c of segment 0 (this pass's input order), one digit
+template <int IN>
+__global__ void __launch_bounds__(kSortThreads) chunk_hist_kernel(SortPass a, uint32_t* __restrict__ chist) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];   // dynamic LDS (the CPU emulation shares it)
+    auto h = (uint32_t(*)[256])smem;                                    // [kSortWaves][256]
+    const uint32_t tid = threadIdx.x, w = tid / kSW;
+    for (uint32_t k = tid; k < kSortWaves * 256; k += kSortThreads) (&h[0][0])[k] = 0;
+    __syncthreads();
+    const uint64_t seg_lo = a.offs[0], seg_hi = a.ends ? a.ends[0] : a.offs[1];
+    const uint64_t lo = seg_lo + (uint64_t)blockIdx.x * kChunk;
+    const uint64_t n = lo >= seg_hi ? 0 : (seg_hi - lo < kChunk ? seg_hi - lo : kChunk);
+    const uint32_t dmask = (1u << a.bits) - 1;
+    for (uint64_t i = tid; i < n; i += kSortThreads) {
+        const uint64_t it = load_item<IN>(a, lo + i, a.end_bit);
+        atomicAdd(&h[w][(uint32_t)(it >> (32 + a.shift)) & dmask], 1u);
+    }
+    __syncthreads();
+    uint32_t v = 0;
+    for (int x = 0; x < kSortWaves; x++) v += h[x][tid];
+    chist[(size_t)blockIdx.x * 256 + tid] = v;
+}
+
+// chunk c's bucket bases: digit d's start in the segment (the counts of smaller digits)
+// plus the counts of digit d in chunks before c; one thread per digit
+__global__ void __launch_bounds__(256) chunk_scan_kernel(uint32_t* __restrict__ chist, uint32_t nchunks) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];   // dynamic LDS (the CPU emulation shares it)
+    uint32_t* scan = (uint32_t*)smem;                                   // [256]
+    const uint32_t d = threadIdx.x;
+    uint32_t run = 0;
+    for (uint32_t c = 0; c < nchunks; c++) {
+        const uint32_t v = chist[(size_t)c * 256 + d];
+        chist[(size_t)c * 256 + d] = run;
+        run += v;
+    }
+    scan[d] = run;
+    __syncthreads();
+    for (uint32_t o = 1; o < 256; o <<= 1) {
+        const uint32_t v = d >= o ? scan[d - o] : 0u;
+        __syncthreads();
+        scan[d] += v;
+        __syncthreads();
+    }
+    const uint32_t base = scan[d] - run;   // the digits below d, over the whole segment
+    for (uint32_t c = 0; c < nchunks; c++) chist[(size_t)c * 256 + d] += base;
+}
+
 template <int IN, int OUT>
 __global__ void __launch_bounds__(kSortThreads) seg_pass_kernel(SortPass a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];   // dynamic LDS (the CPU emulation shares it)
@@ -113,20 +167,30 @@ __global__ void __launch_bounds__(kSortThreads) seg_pass_kernel(SortPass a) {
     uint32_t* scan = loff + 256;
     auto cnt = (uint32_t(*)[256])(scan + 256);                           // [kSortWaves][256]
     const uint32_t tid = threadIdx.x, w = tid / kSW, lane = tid % kSW;
-    const uint32_t s = blockIdx.x;
-    const uint64_t lo = a.offs[s], n = (a.ends ? a.ends[s] : a.offs[s + 1]) - lo;
-    const uint32_t nb = 1u << a.bits, dmask = nb - 1;
-    // bucket bases of this stream: exclusive scan of its histogram (Hillis-Steele in LDS)
-    const uint32_t hv = tid < nb ? a.hist[((size_t)s * kMaxPasses + a.pass) * 256 + tid] : 0u;
-    scan[tid] = hv;
-    __syncthreads();
-    for (uint32_t o = 1; o < 256; o <<= 1) {
-        const uint32_t v = tid >= o ? scan[tid - o] : 0u;
-        __syncthreads();
-        scan[tid] += v;
-        __syncthreads();
+    const uint32_t s = a.cbase ? 0u : blockIdx.x;
+    const uint64_t seg_lo = a.offs[s], seg_hi = a.ends ? a.ends[s] : a.offs[s + 1];
+    uint64_t lo = seg_lo, n = seg_hi - seg_lo;
+    if (a.cbase) {   // chunked: this block's chunk of segment 0, its bases from chunk_scan_kernel
+        lo = seg_lo + (uint64_t)blockIdx.x * kChunk;
+        if (lo >= seg_hi) return;   // the whole block: past the segment's end
+        n = seg_hi - lo < kChunk ? seg_hi - lo : kChunk;
     }
-    base[tid] = scan[tid] - hv;
+    const uint32_t nb = 1u << a.bits, dmask = nb - 1;
+    if (a.cbase) {
+        base[tid] = a.cbase[(size_t)blockIdx.x * 256 + tid];
+    } else {
+        // bucket bases of this stream: exclusive scan of its histogram (Hillis-Steele in LDS)
+        const uint32_t hv = tid < nb ? a.hist[((size_t)s * kMaxPasses + a.pass) * 256 + tid] : 0u;
+        scan[tid] = hv;
+        __syncthreads();
+        for (uint32_t o = 1; o < 256; o <<= 1) {
+            const uint32_t v = tid >= o ? scan[tid - o] : 0u;
+            __syncthreads();
+            scan[tid] += v;
+            __syncthreads();
+        }
+        base[tid] = scan[tid] - hv;
+    }
     for (uint32_t x = 0; x < kSortWaves; x++) cnt[x][tid] = 0;
     __syncthreads();
     for (uint64_t t0 = 0; t0 < n; t0 += kSortTile) {
@@ -184,7 +248,7 @@ __global__ void __launch_bounds__(kSortThreads) seg_pass_kernel(SortPass a) {
         for (uint32_t j = tid; j < tn; j += kSortThreads) {
             const uint64_t it = tile[j];
             const uint32_t d = (uint32_t)(it >> (32 + a.shift)) & dmask;
-            const uint64_t dst = (OUT != SK_PACKED && a.dofs ? a.dofs[s] : lo) + base[d] + (j - loff[d]);
+            const uint64_t dst = (OUT != SK_PACKED && a.dofs ? a.dofs[s] : seg_lo) + base[d] + (j - loff[d]);
             if (OUT == SK_PACKED) {
                 ((uint64_t*)a.kout)[dst] = it;
             } else {
@@ -204,8 +268,12 @@ __global__ void __launch_bounds__(kSortThreads) seg_pass_kernel(SortPass a) {
 }
 
 template <int IN, int OUT>
-static void launch_pass(const SortPass& p, int nstreams, hipStream_t st) {
-    hipLaunchKernelGGL((seg_pass_kernel<IN, OUT>), dim3(nstreams), dim3(kSortThreads), kPassLds, st, p);
+static void launch_pass(const SortPass& p, int nblocks, hipStream_t st, uint32_t* chist) {
+    if (p.cbase) {   // chunked: this pass's per-chunk histograms and bases first
+        hipLaunchKernelGGL((chunk_hist_kernel<IN>), dim3(nblocks), dim3(kSortThreads), (size_t)kSortWaves * 256 * 4, st, p, chist);
+        hipLaunchKernelGGL(chunk_scan_kernel, dim3(1), dim3(256), 256 * 4, st, chist, (uint32_t)nblocks);
+    }
+    hipLaunchKernelGGL((seg_pass_kernel<IN, OUT>), dim3(nblocks), dim3(kSortThreads), kPassLds, st, p);
 }
 
 // Stable sort of every stream's items by the low end_bit bits of their keys.
@@ -228,8 +296,17 @@ int seg_radix_sort(Ctx* ctx, bool key64, const void* kin, const uint32_t* vin, v
     }
     SortPass p{};
     p.kin = kin; p.vin = vin; p.offs = d_offs; p.ends = d_ends; p.dofs = d_dofs; p.hist = hist; p.end_bit = (uint32_t)end_bit;
-    if (key64) hipLaunchKernelGGL((seg_hist_kernel<SK_KEY64>), dim3(nstreams), dim3(kSortThreads), kHistLds, st, p, npass, widths, hist);
-    else hipLaunchKernelGGL((seg_hist_kernel<SK_KEY32>), dim3(nstreams), dim3(kSortThreads), kHistLds, st, p, npass, widths, hist);
+    // one long segment: chunked (n bounds the segment; blocks past its end exit), the chunk
+    // histograms and bases in `hist` (sort_hist_words)
+    const bool chunked = nstreams == 1 && n > 4 * kChunk;
+    const int nblocks = chunked ? (int)((n + kChunk - 1) / kChunk) : nstreams;
+    if (chunked) {
+        p.cbase = hist;
+    } else if (key64) {
+        hipLaunchKernelGGL((seg_hist_kernel<SK_KEY64>), dim3(nstreams), dim3(kSortThreads), kHistLds, st, p, npass, widths, hist);
+    } else {
+        hipLaunchKernelGGL((seg_hist_kernel<SK_KEY32>), dim3(nstreams), dim3(kSortThreads), kHistLds, st, p, npass, widths, hist);
+    }
     uint32_t shift = 0;
     uint64_t* bufs[2] = {tmp_a, tmp_b};
     for (uint32_t q = 0; q < npass; q++) {
@@ -243,18 +320,27 @@ int seg_radix_sort(Ctx* ctx, bool key64, const void* kin, const uint32_t* vin, v
         x.vout = vout;
         const int in = first ? (key64 ? SK_KEY64 : SK_KEY32) : SK_PACKED;
         const int out = last ? (key64 ? SK_KEY64 : SK_KEY32) : SK_PACKED;
-        if (in == SK_KEY64 && out == SK_KEY64) launch_pass<SK_KEY64, SK_KEY64>(x, nstreams, st);
-        else if (in == SK_KEY64) launch_pass<SK_KEY64, SK_PACKED>(x, nstreams, st);
-        else if (in == SK_KEY32 && out == SK_KEY32) launch_pass<SK_KEY32, SK_KEY32>(x, nstreams, st);
-        else if (in == SK_KEY32) launch_pass<SK_KEY32, SK_PACKED>(x, nstreams, st);
-        else if (out == SK_KEY64) launch_pass<SK_PACKED, SK_KEY64>(x, nstreams, st);
-        else if (out == SK_KEY32) launch_pass<SK_PACKED, SK_KEY32>(x, nstreams, st);
-        else launch_pass<SK_PACKED, SK_PACKED>(x, nstreams, st);
+        uint32_t* ch = chunked ? hist : nullptr;
+        if (in == SK_KEY64 && out == SK_KEY64) launch_pass<SK_KEY64, SK_KEY64>(x, nblocks, st, ch);
+        else if (in == SK_KEY64) launch_pass<SK_KEY64, SK_PACKED>(x, nblocks, st, ch);
+        else if (in == SK_KEY32 && out == SK_KEY32) launch_pass<SK_KEY32, SK_KEY32>(x, nblocks, st, ch);
+        else if (in == SK_KEY32) launch_pass<SK_KEY32, SK_PACKED>(x, nblocks, st, ch);
+        else if (out == SK_KEY64) launch_pass<SK_PACKED, SK_KEY64>(x, nblocks, st, ch);
+        else if (out == SK_KEY32) launch_pass<SK_PACKED, SK_KEY32>(x, nblocks, st, ch);
+        else launch_pass<SK_PACKED, SK_PACKED>(x, nblocks, st, ch);
         shift += x.bits;
     }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return ctx->fail(LZMA_E_DEVICE, "seg_radix_sort: %s", hipGetErrorString(e));
     return LZMA_OK;
+}
+
+// u32 words the `hist` argument of seg_radix_sort needs: every pass's histogram per stream,
+// or, for one long segment (chunked), the bases of every chunk
+size_t sort_hist_words(uint64_t n, int nstreams) {
+    const size_t seg = (size_t)nstreams * kMaxPasses * 256;
+    const size_t chunked = nstreams == 1 ? (size_t)((n + kChunk - 1) / kChunk) * 256 : 0;
+    return seg > chunked ? seg : chunked;
 }
 
 }  // namespace lzg
