@@ -597,13 +597,13 @@ _KERNEL_OF = {"enc_parse": "enc_kernel", "dec_stream": "dec_kernel", "mf_walk": 
 
 
 def _profile_prefix(wl):
-    """round 5's summaries (tools/r05/prof.sh, DATA=bench / DATA=text) of this same
+    """round 6's summaries (tools/r06/prof.sh, DATA=bench / DATA=text) of this same
     workload, taken at the kernels this tree builds"""
-    return "r05/text_" if wl.get("data") == "text" else "r05/"
+    return "r06/text_" if wl.get("data") == "text" else "r06/"
 
 
 def _profile(name, wl):
-    """A committed per-kernel summary from profiles/ (written by tools/r05/prof.sh
+    """A committed per-kernel summary from profiles/ (written by tools/r06/prof.sh
     over this same workload), or None when absent or taken on another workload."""
     path = os.path.join(REPO, "profiles", _profile_prefix(wl) + name)
     if not os.path.exists(path):
