@@ -548,8 +548,11 @@ __global__ void __launch_bounds__(64) LZG_WALK_ATTR mf_walk_kernel(const uint8_t
         bool p0_self = true, p1_self = true;   // ptr0 = son[2i + 1] (s1), ptr1 = son[2i] (s0)
         uint64_t* ptr0 = &nodes[i].s1;
         uint64_t* ptr1 = &nodes[i].s0;
-        auto put0 = [&](uint64_t v) { if (p0_self) self.s1 = v; else *ptr0 = v; };
-        auto put1 = [&](uint64_t v) { if (p1_self) self.s0 = v; else *ptr1 = v; };
+        // the chain's last member: no later member walks the tree, so its links and its own
+        // node are never read -- its walk stores only the match list
+        const bool live_tree = i + 1 < end;
+        auto put0 = [&](uint64_t v) { if (p0_self) self.s1 = v; else if (live_tree) *ptr0 = v; };
+        auto put1 = [&](uint64_t v) { if (p1_self) self.s0 = v; else if (live_tree) *ptr1 = v; };
         uint64_t cur_idx = i - 1;           // sorted index of the head (valid while cur_match != 0)
         uint32_t len0 = a.direct_bytes, len1 = a.direct_bytes;
         if (!BT4 && cur_match > match_min) {   // BT2 direct byte check, BinTree.java:218-226
@@ -609,7 +612,7 @@ __global__ void __launch_bounds__(64) LZG_WALK_ATTR mf_walk_kernel(const uint8_t
                 ml += common_len(sb + from - d1, sb + from, 0, (uint32_t)lim);
             }
         }
-        nodes[i] = self;
+        if (live_tree) nodes[i] = self;
         head = self;
         // outputs are touched once: non-temporal, so the stream's nodes and bytes keep the L2
         store_rec<PairT>(recs + g * rec_vecs<PairT>(), q0, q1, q2, q3, cnt | (ml << 16));

@@ -36,7 +36,8 @@ def main():
     st = torch.cuda.current_stream(dev).cuda_stream
     out = {"data": kind, "streams": n, "chunk": chunk}
     rows = (("all (full encode)", None), ("all", "0,4294967295"), ("< 256", "0,255"),
-            (">= 256", "256,4294967295"), (">= 1024", "1024,4294967295"), ("none", "4294967295,4294967295"))
+            (">= 256", "256,4294967295"), (">= 1024", "1024,4294967295"), ("== 1", "1,1"), (">= 2", "2,4294967295"),
+            ("none", "4294967295,4294967295"))
     if os.environ.get("WALK_FULL_ONLY"):   # a product-form library (no LZG_WALK_ONLY): full encodes only
         rows = rows[:1]
     for name, rng in rows:
