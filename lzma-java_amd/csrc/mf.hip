@@ -52,7 +52,6 @@ __global__ void __launch_bounds__(256) mf_keys_kernel(const uint8_t* __restrict_
     while (s + 1 < nstreams && offs[s + 1] <= g) s++;
     if (g < total) {
         uint64_t base = offs[s], n = offs[s + 1] - base, p = g - base;
-        a.vals[g] = (uint32_t)g;
         uint64_t rem = n - p;
         uint32_t len_limit = rem < a.fb ? (uint32_t)rem : a.fb;
         if (len_limit < a.min_match_check) {   // BinTree.java:153-162: no insertion
@@ -221,13 +220,13 @@ __device__ __forceinline__ uint32_t chain_order_key(uint32_t len) {
 
 // The chain (bucket) lists of one stream, one workgroup per stream: chain k of the
 // stream (its k-th bucket in sorted order) at index lo + k gets its first sorted index,
-// its length, its walk-order key and its own index (for the order sort);
+// its length and its walk-order key (the order sort takes index lo + k as the value);
 // seg_end[s] = lo + chains.
 // Sentinel keys (no insertion) sort last in their stream and form no chain.
 constexpr uint32_t kChainThreads = 256, kChainItems = 4;
 __global__ void __launch_bounds__(kChainThreads) mf_chains_kernel(const uint64_t* __restrict__ offs, const uint64_t* __restrict__ keys,
                                                                    uint32_t* __restrict__ chain_start, uint32_t* __restrict__ chain_len,
-                                                                   uint32_t* __restrict__ okey, uint32_t* __restrict__ cidx,
+                                                                   uint32_t* __restrict__ okey,
                                                                    uint64_t* __restrict__ seg_end, uint32_t long_min,
                                                                    uint32_t* __restrict__ cls, uint32_t* __restrict__ long_raw) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];   // dynamic LDS (the CPU emulation shares it)
@@ -275,7 +274,6 @@ __global__ void __launch_bounds__(kChainThreads) mf_chains_kernel(const uint64_t
         const uint32_t len = en - st;
         chain_len[lo + c] = len;
         okey[lo + c] = chain_order_key(len);
-        cidx[lo + c] = (uint32_t)(lo + c);
         if (len >= long_min) {
             long_raw[atomicAdd(&cls[64], 1u)] = (uint32_t)(lo + c);
             atomicAdd(&cls[31 - __clz((int)len)], 1u);
@@ -643,7 +641,7 @@ static MfArgs mf_args(const Derived& d, const MfBuffers& w, uint64_t total, int 
         unsigned lo = 0, hi = 0xFFFFFFFFu;
         if (sscanf(e, "%u,%u", &lo, &hi) >= 1) { a.walk_lo = lo; a.walk_hi = hi; }
     }
-    a.k4 = w.k4; a.k3 = (uint32_t*)w.k3; a.k2 = (uint32_t*)w.k2; a.vals = w.vals; a.mrec = w.pairs; a.rec_vecs = wide_pairs ? rec_vecs<uint64_t>() : rec_vecs<uint32_t>(); a.prev3 = w.prev3;
+    a.k4 = w.k4; a.k3 = w.k3; a.k2 = w.k2; a.mrec = w.pairs; a.rec_vecs = wide_pairs ? rec_vecs<uint64_t>() : rec_vecs<uint32_t>(); a.prev3 = w.prev3;
     return a;
 }
 
@@ -677,7 +675,7 @@ int mf_front(Ctx* ctx, const Derived& d, const uint8_t* in, const uint64_t* d_of
         const unsigned prev_grid = (unsigned)(((total + B - 1) / B + 7) & ~7ull);   // total < 2^32: fits
         {
             TimedLaunch tl(ctx, "mf_sort", st);
-            if ((rc = seg_radix_sort(ctx, false, w.k3, w.vals, w.ks, w.vs, w.son, w.son + total, w.hist, total, d_offs, nstreams, 16, st))) return rc;
+            if ((rc = seg_radix_sort(ctx, false, w.k3, nullptr, w.ks, w.vs, w.son, w.son + total, w.hist, total, d_offs, nstreams, 16, st))) return rc;
         }
         hipLaunchKernelGGL(mf_prev_kernel, dim3(prev_grid), dim3(B), 0, st, (const uint32_t*)w.ks, w.vs, total, w.prev3);
         {   // after mf_prev: the walk-input records carry both candidates
@@ -688,24 +686,24 @@ int mf_front(Ctx* ctx, const Derived& d, const uint8_t* in, const uint64_t* d_of
     }
     {
         TimedLaunch tl(ctx, "mf_sort", st);
-        if ((rc = seg_radix_sort(ctx, true, w.k4, w.vals, w.ks, w.vs, w.son, w.son + total, w.hist, total, d_offs, nstreams,
+        if ((rc = seg_radix_sort(ctx, true, w.k4, nullptr, w.ks, w.vs, w.son, w.son + total, w.hist, total, d_offs, nstreams,
                                  (int)(bt4 ? d.hash_bits : 16), st))) return rc;
     }
     // chain lists and walk order: stream by stream (cache locality), longest chains first
     // within a stream (lanes of one wave walk similar-length buckets). The k2/k3 key
     // arrays are dead here and hold the order keys.
-    uint32_t* okey = (uint32_t*)w.k2;
-    uint32_t* okey_sorted = (uint32_t*)w.k3;
+    uint32_t* okey = w.k2;
+    uint32_t* okey_sorted = w.k3;
     uint32_t* long_raw = (uint32_t*)w.k4;   // dead since the hash4 sort
     const uint32_t long_min = mf_long_min();
     {
         TimedLaunch tl(ctx, "mf_sort", st);
         hipMemsetAsync(w.cls, 0, 96 * sizeof(uint32_t), st);
         hipLaunchKernelGGL(mf_chains_kernel, dim3(nstreams), dim3(kChainThreads), (2 * (kChainThreads / 64) + 2) * 4, st, d_offs, w.ks,
-                           w.chain_start, w.chain_len, okey, w.chain_idx, w.seg_end, long_min, w.cls, long_raw);
+                           w.chain_start, w.chain_len, okey, w.seg_end, long_min, w.cls, long_raw);
         hipLaunchKernelGGL(mf_chain_scan_kernel, dim3(1), dim3(kChainThreads), (kChainThreads / 64 + 2) * 4, st, d_offs, w.seg_end,
                            nstreams, w.chain_offs);
-        if ((rc = seg_radix_sort(ctx, false, okey, w.chain_idx, okey_sorted, w.chain_order, w.son, w.son + total, w.hist, total,
+        if ((rc = seg_radix_sort(ctx, false, okey, nullptr, okey_sorted, w.chain_order, w.son, w.son + total, w.hist, total,
                                  d_offs, nstreams, 8, st, w.seg_end, w.chain_offs))) return rc;
     }
     return LZMA_OK;
@@ -739,7 +737,8 @@ int mf_walk_launch(Ctx* ctx, const Derived& d, const uint8_t* in, const uint64_t
     MfArgs a = mf_args(d, w, total, nstreams, wide_pairs);
     const bool bt4 = d.hash_array != 0;
     const unsigned B = 256;
-    uint32_t* long_raw = (uint32_t*)w.k4;
+    uint32_t* long_raw = (uint32_t*)w.k4;            // k4 is dead since the hash4 sort: the long chains
+    uint32_t* long_list = (uint32_t*)w.k4 + total;   // unordered, then in class order
     const uint32_t long_min = mf_long_min();
     uint64_t* p_cnt = pin_slot(ctx, slot);
     const uint64_t nchains = p_cnt[0];
@@ -752,7 +751,7 @@ int mf_walk_launch(Ctx* ctx, const Derived& d, const uint8_t* in, const uint64_t
         TimedLaunch tl(ctx, "mf_sort", st);
         hipLaunchKernelGGL(mf_long_offsets_kernel, dim3(1), dim3(64), 0, st, w.cls);
         hipLaunchKernelGGL(mf_long_scatter_kernel, dim3((n_long + B - 1) / B), dim3(B), 0, st, long_raw, n_long, w.chain_len, w.cls,
-                           w.long_list);
+                           long_list);
     }
     hipMemsetAsync(w.ovf_used, 0, sizeof(unsigned long long), st);
     hipMemsetAsync(w.err, 0, sizeof(int), st);
@@ -765,11 +764,11 @@ int mf_walk_launch(Ctx* ctx, const Derived& d, const uint8_t* in, const uint64_t
         // experiment: dynamic LDS per wave caps the waves per CU (L2 working set)
         static const size_t walk_lds = exp_env("LZG_WALK_LDS") ? (size_t)atoi(exp_env("LZG_WALK_LDS")) : 0;
         if (wide_pairs) {
-            if (bt4) hipLaunchKernelGGL((mf_walk_kernel<uint64_t, true>), dim3(grid), dim3(WB), walk_lds, st, in, d_offs, w.ks, w.vs, w.chain_order, w.chain_start, w.chain_len, nchains, w.long_list, (uint64_t)n_long, long_blocks, long_min, a, (WNode*)w.son, w.pairs, w.ovf_off, (uint64_t*)w.ovf, w.ovf_used, w.ovf_cap, ovf_stride(d.fb), w.err);
-            else hipLaunchKernelGGL((mf_walk_kernel<uint64_t, false>), dim3(grid), dim3(WB), walk_lds, st, in, d_offs, w.ks, w.vs, w.chain_order, w.chain_start, w.chain_len, nchains, w.long_list, (uint64_t)n_long, long_blocks, long_min, a, (WNode*)w.son, w.pairs, w.ovf_off, (uint64_t*)w.ovf, w.ovf_used, w.ovf_cap, ovf_stride(d.fb), w.err);
+            if (bt4) hipLaunchKernelGGL((mf_walk_kernel<uint64_t, true>), dim3(grid), dim3(WB), walk_lds, st, in, d_offs, w.ks, w.vs, w.chain_order, w.chain_start, w.chain_len, nchains, long_list, (uint64_t)n_long, long_blocks, long_min, a, (WNode*)w.son, w.pairs, w.ovf_off, (uint64_t*)w.ovf, w.ovf_used, w.ovf_cap, ovf_stride(d.fb), w.err);
+            else hipLaunchKernelGGL((mf_walk_kernel<uint64_t, false>), dim3(grid), dim3(WB), walk_lds, st, in, d_offs, w.ks, w.vs, w.chain_order, w.chain_start, w.chain_len, nchains, long_list, (uint64_t)n_long, long_blocks, long_min, a, (WNode*)w.son, w.pairs, w.ovf_off, (uint64_t*)w.ovf, w.ovf_used, w.ovf_cap, ovf_stride(d.fb), w.err);
         } else {
-            if (bt4) hipLaunchKernelGGL((mf_walk_kernel<uint32_t, true>), dim3(grid), dim3(WB), walk_lds, st, in, d_offs, w.ks, w.vs, w.chain_order, w.chain_start, w.chain_len, nchains, w.long_list, (uint64_t)n_long, long_blocks, long_min, a, (WNode*)w.son, w.pairs, w.ovf_off, (uint32_t*)w.ovf, w.ovf_used, w.ovf_cap, ovf_stride(d.fb), w.err);
-            else hipLaunchKernelGGL((mf_walk_kernel<uint32_t, false>), dim3(grid), dim3(WB), walk_lds, st, in, d_offs, w.ks, w.vs, w.chain_order, w.chain_start, w.chain_len, nchains, w.long_list, (uint64_t)n_long, long_blocks, long_min, a, (WNode*)w.son, w.pairs, w.ovf_off, (uint32_t*)w.ovf, w.ovf_used, w.ovf_cap, ovf_stride(d.fb), w.err);
+            if (bt4) hipLaunchKernelGGL((mf_walk_kernel<uint32_t, true>), dim3(grid), dim3(WB), walk_lds, st, in, d_offs, w.ks, w.vs, w.chain_order, w.chain_start, w.chain_len, nchains, long_list, (uint64_t)n_long, long_blocks, long_min, a, (WNode*)w.son, w.pairs, w.ovf_off, (uint32_t*)w.ovf, w.ovf_used, w.ovf_cap, ovf_stride(d.fb), w.err);
+            else hipLaunchKernelGGL((mf_walk_kernel<uint32_t, false>), dim3(grid), dim3(WB), walk_lds, st, in, d_offs, w.ks, w.vs, w.chain_order, w.chain_start, w.chain_len, nchains, long_list, (uint64_t)n_long, long_blocks, long_min, a, (WNode*)w.son, w.pairs, w.ovf_off, (uint32_t*)w.ovf, w.ovf_used, w.ovf_cap, ovf_stride(d.fb), w.err);
         }
     }
     LZG_TRACE(ctx, st, "mf_walk done (%llu chains)", (unsigned long long)nchains);

@@ -40,7 +40,7 @@ struct MfArgs {
     uint64_t cyc_size;
     uint64_t* k4;
     uint32_t *k3, *k2;            // (stream << 16 | hash3), (stream << 10 | hash2): < 2^30 for <= 16384 streams
-    uint32_t *vals, *prev3;       // prev3: hash3 "last occurrence" by position (mf_prev_kernel)
+    uint32_t* prev3;              // hash3 "last occurrence" by position (mf_prev_kernel)
     v4u32* mrec;                  // per-position match-list records (lzma_common.h store_rec)
     uint32_t walk_lo, walk_hi;    // experiment hook (LZG_WALK_ONLY): walk only chains of length in [lo, hi]
     uint64_t total;               // positions of the pass (every chain, sorted index and position is below it)
@@ -48,10 +48,10 @@ struct MfArgs {
 };
 
 struct MfBuffers {
-    uint64_t *k4, *k3, *k2, *ks;
-    uint32_t *vals, *vs, *prev3;
-    uint8_t* flag;
-    uint32_t *chain_start, *chain_len, *long_list, *chain_idx, *chain_order;
+    uint64_t *k4, *ks;            // k4's memory holds the long-chain lists after the hash4 sort
+    uint32_t *k3, *k2;            // also the walk-order keys (k2) and their sorted copy (k3)
+    uint32_t *vs, *prev3;
+    uint32_t *chain_start, *chain_len, *chain_order;
     uint32_t* cls;                // long chains per length class [32], the scatter cursors [32], the long count [1]
     uint64_t* son;                // walk tree nodes (mf.hip WNode, 32 B per position: links + 16-byte prefix);
                                   // before the walk, the sorts' ping-pong buffers

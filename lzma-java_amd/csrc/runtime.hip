@@ -191,12 +191,13 @@ static int pass_carve(Ctx* ctx, EncPass& P) {
     const uint64_t T = P.total;
     const int ns = P.ns;
     auto phase1 = [&](Carver& c, MfBuffers& w) {   // buffers only the match finder uses
-        w.k4 = c.take<uint64_t>(T); w.k3 = c.take<uint64_t>(T); w.k2 = c.take<uint64_t>(T); w.ks = c.take<uint64_t>(T);
-        w.vals = c.take<uint32_t>(T); w.vs = c.take<uint32_t>(T);
+        // positions need no array of their own (the sorts' first pass takes the index), nor do
+        // the chains' own indices; the long-chain lists live in k4's memory after the hash4 sort
+        w.k4 = c.take<uint64_t>(T); w.k3 = c.take<uint32_t>(T); w.k2 = c.take<uint32_t>(T); w.ks = c.take<uint64_t>(T);
+        w.vs = c.take<uint32_t>(T);
         w.prev3 = c.take<uint32_t>(T);
-        w.flag = c.take<uint8_t>(T);
-        w.chain_start = c.take<uint32_t>(T); w.chain_len = c.take<uint32_t>(T); w.long_list = c.take<uint32_t>(T);
-        w.chain_idx = c.take<uint32_t>(T); w.chain_order = c.take<uint32_t>(T);
+        w.chain_start = c.take<uint32_t>(T); w.chain_len = c.take<uint32_t>(T);
+        w.chain_order = c.take<uint32_t>(T);
         w.cls = c.take<uint32_t>(96);
         w.son = c.take<uint64_t>(4 * T);   // mf.hip WNode: 32 bytes per position
         w.hist = c.take<uint32_t>(sort_hist_words(T, ns));

@@ -49,7 +49,7 @@ constexpr uint64_t kChunk = 1u << 16;
 
 struct SortPass {
     const void* kin;          // SK_KEY64 / SK_KEY32 keys, or packed items (SK_PACKED)
-    const uint32_t* vin;      // positions (first pass only)
+    const uint32_t* vin;      // values (first pass only); null: each item's own index
     void* kout;               // packed items, or the final keys
     uint32_t* vout;           // final positions (last pass only)
     const uint64_t* offs;     // stream offsets (nstreams + 1), relative to the pass
@@ -78,7 +78,7 @@ __device__ __forceinline__ uint64_t load_item(const SortPass& a, uint64_t i, uin
         sent = k == ~0u;
         h = k & mask;
     }
-    return ((uint64_t)(h | (sent << 31)) << 32) | a.vin[i];
+    return ((uint64_t)(h | (sent << 31)) << 32) | (a.vin ? a.vin[i] : (uint32_t)i);   // no vin: the index
 }
 
 // every pass's histogram of one stream (one read sweep); per-wave LDS copies keep
