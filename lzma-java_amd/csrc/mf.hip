@@ -205,6 +205,8 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* wsum) 
 // within a class is free: a chain's walk touches only its own positions, nodes
 // and records. mf_chains_kernel lists them (unordered) and counts the classes.
 constexpr uint32_t kWalkLong = 256;
+constexpr uint32_t kWalkCapPct = 8;          // long chains' share of the positions (lower bound) that caps the walk
+constexpr size_t kWalkCapLds = 40 * 1024;    // LDS per 64-lane block under the cap: 4 blocks per CU
 
 // Walk-order key of a chain: longest first (lanes of one wave walk similar-length
 // buckets); exact below 128, then 8 steps per doubling. Only the order depends on it.
@@ -710,19 +712,24 @@ int mf_front(Ctx* ctx, const Derived& d, const uint8_t* in, const uint64_t* d_of
 }
 
 // pinned words of a slot: [0] chain count, [1] long-chain count, [2] the walk's verdict
-static uint64_t* pin_slot(Ctx* ctx, int slot) { return ctx->pin_mf.as<uint64_t>() + 4 * slot; }
+// pinned words of a slot: [0] chain count, [1] long-chain count, [2] the walk's verdict,
+// [4, 20): the long chains per length class (32 u32, mf_chains_kernel's cls[0..31])
+constexpr int kPinSlotWords = 20;
+static uint64_t* pin_slot(Ctx* ctx, int slot) { return ctx->pin_mf.as<uint64_t>() + kPinSlotWords * slot; }
 
 int mf_count_enqueue(Ctx* ctx, const MfBuffers& w, int nstreams, hipStream_t st, int slot) {
-    if (!ctx->pin_mf.ensure(64)) return ctx->fail(LZMA_E_NOMEM, "pinned staging");
+    if (!ctx->pin_mf.ensure(2 * kPinSlotWords * sizeof(uint64_t))) return ctx->fail(LZMA_E_NOMEM, "pinned staging");
     if (!ctx->cnt_done[slot] && hipEventCreateWithFlags(&ctx->cnt_done[slot], hipEventDisableTiming) != hipSuccess)
         return ctx->fail(LZMA_E_DEVICE, "chain-count event");
     uint64_t* p_cnt = pin_slot(ctx, slot);
     p_cnt[0] = p_cnt[1] = 0;
+    for (int k = 4; k < kPinSlotWords; k++) p_cnt[k] = 0;
     p_cnt[2] = 0;   // the walk's verdict (no walk: none)
     // sizes the walk grid: one host round trip per pass (pinned: see HostBuf)
     if (w.chain_offs &&
         (hipMemcpyAsync(p_cnt, w.chain_offs + nstreams, 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
-         hipMemcpyAsync(p_cnt + 1, w.cls + 64, 4, hipMemcpyDeviceToHost, st) != hipSuccess))
+         hipMemcpyAsync(p_cnt + 1, w.cls + 64, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+         hipMemcpyAsync(p_cnt + 4, w.cls, 32 * sizeof(uint32_t), hipMemcpyDeviceToHost, st) != hipSuccess))
         return ctx->fail(LZMA_E_DEVICE, "mf: chain count: %s", hipGetErrorString(hipGetLastError()));
     if (hipEventRecord(ctx->cnt_done[slot], st) != hipSuccess)
         return ctx->fail(LZMA_E_DEVICE, "mf: chain count: %s", hipGetErrorString(hipGetLastError()));
@@ -761,8 +768,17 @@ int mf_walk_launch(Ctx* ctx, const Derived& d, const uint8_t* in, const uint64_t
         const unsigned long_blocks = (unsigned)(((n_long + WB - 1) / WB + 7) & ~7ull);
         unsigned grid = (unsigned)((nchains + WB - 1) / WB);
         grid = ((grid + 7) & ~7u) + long_blocks;   // multiples of 8 (XCD-aware mapping in mf_walk_kernel)
-        // experiment: dynamic LDS per wave caps the waves per CU (L2 working set)
-        static const size_t walk_lds = exp_env("LZG_WALK_LDS") ? (size_t)atoi(exp_env("LZG_WALK_LDS")) : 0;
+        // Waves per CU capped through dynamic LDS when long chains hold many of the positions:
+        // a long chain's tree steps read 32-byte nodes all over its bucket's run, and with every
+        // wave of the launch resident those reads thrash the XCD's L2; one walk wave per SIMD
+        // lets them hit. TEXT (26 % of the positions in chains of 256 or more): walk 763 -> 696 ms;
+        // BENCH (1.6 %) keeps every wave (a cap of 8 per CU cost it 10 %)
+        // (profiles/r06/walk_split_text_caps.txt, ab/walk_cap_*.jsonl). LZG_WALK_LDS overrides (experiments).
+        uint64_t long_members = 0;   // a lower bound: 2^class per chain
+        const uint32_t* lcls = (const uint32_t*)(p_cnt + 4);
+        for (int k = 0; k < 32; k++) long_members += (uint64_t)lcls[k] << k;
+        const size_t walk_lds = exp_env("LZG_WALK_LDS") ? (size_t)atoi(exp_env("LZG_WALK_LDS"))
+                                : (long_members * 100 >= total * (uint64_t)kWalkCapPct ? kWalkCapLds : 0);
         if (wide_pairs) {
             if (bt4) hipLaunchKernelGGL((mf_walk_kernel<uint64_t, true>), dim3(grid), dim3(WB), walk_lds, st, in, d_offs, w.ks, w.vs, w.chain_order, w.chain_start, w.chain_len, nchains, long_list, (uint64_t)n_long, long_blocks, long_min, a, (WNode*)w.son, w.pairs, w.ovf_off, (uint64_t*)w.ovf, w.ovf_used, w.ovf_cap, ovf_stride(d.fb), w.err);
             else hipLaunchKernelGGL((mf_walk_kernel<uint64_t, false>), dim3(grid), dim3(WB), walk_lds, st, in, d_offs, w.ks, w.vs, w.chain_order, w.chain_start, w.chain_len, nchains, long_list, (uint64_t)n_long, long_blocks, long_min, a, (WNode*)w.son, w.pairs, w.ovf_off, (uint64_t*)w.ovf, w.ovf_used, w.ovf_cap, ovf_stride(d.fb), w.err);
