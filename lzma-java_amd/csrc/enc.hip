@@ -209,6 +209,14 @@ struct Enc {
     const PairT* mdp;         // the current position's pairs (packed): its ring slot, or md_buf
     PairT* md_buf;            // a copy when the list is longer than the inline pairs or is clamped
     uint8_t* win;             // gather window: the cur side's bytes at offsets -1 .. kGW - 2 (aliased by tp)
+#ifdef LZG_EXP_WTILE
+    // recent-window tile (few streams per CU): an LDS ring of the stream's bytes [wt_lo, wt_hi),
+    // wt_hi - wt_lo <= kWT, kept ahead of the gather; a gathered side whose 64 bytes lie inside
+    // it reads LDS instead of the stream (InWindow.GetMatchLen, InWindow.java:120-134)
+    static constexpr uint32_t kWT = LZG_EXP_WTILE;
+    uint8_t* wt;
+    uint32_t wt_lo, wt_hi;
+#endif
     uint32_t* ring_info;      // [kRing]
     PairT* ring_pairs;        // [kRing * kInlinePairs]
     uint32_t* o_price;        // _optimum SoA, [kOptLds] each (+ the sink entry, + kFarEntry)
@@ -462,11 +470,47 @@ struct Enc {
     // equality masks per side (bit o+1 = bytes equal at offset o), keeps the three
     // bytes the position step prices its literal with in scalars and the cur side's
     // bytes in LDS (two-step literals). Compares past the window fall back to match_len.
+#ifdef LZG_EXP_WTILE
+    // the tile's top kept at least 64 bytes past the gather's last offset (1 KiB per refill,
+    // one 16-byte load per lane); a resumed slice starts the tile at its own position
+    FI void wt_fill() {
+        const uint32_t want = mfpos + 128u;
+        if (wt_hi >= want || wt_hi >= n) return;
+        if (wt_hi + kWT <= mfpos) { wt_hi = mfpos & ~1023u; wt_lo = wt_hi; }
+        do {
+            const uint32_t o = wt_hi + lane_id() * 16u;
+            const v4u32 x = __builtin_amdgcn_raw_buffer_load_b128(inb, o, 0, 0);
+            *(v4u32*)(wt + (o & (kWT - 1))) = x;
+            wt_hi += 1024u;
+        } while (wt_hi < want && wt_hi < n);
+        if (wt_hi - wt_lo > kWT) wt_lo = wt_hi - kWT;
+        LANE_FENCE();
+    }
+    // the side at distance d (0 = cur) lies in the tile for all 64 lanes; the top is capped at
+    // the last whole 16-byte load inside the stream
+    FI bool wt_has(uint32_t q0, uint32_t d) const {
+        const uint32_t top = wt_hi < (n & ~15u) ? wt_hi : (n & ~15u);
+        return q0 >= d + wt_lo && q0 + 63u - d < top;
+    }
+    FI uint32_t side_byte(uint32_t q, uint32_t d, bool tile) const {
+        return tile ? (uint32_t)wt[(q - d) & (kWT - 1)] : in_byte(q - d);
+    }
+#endif
     FI void gather(bool with_pairs) {
         gp = mfpos - 1;
         const uint32_t d0 = rp0 + 1, d1 = rp1 + 1, d2 = rp2 + 1, d3 = rp3 + 1;
         const uint32_t e0 = num_pairs > 0 ? md_d(0) + 1 : d0, e1 = num_pairs > 1 ? md_d(1) + 1 : d0;
         uint32_t va[kGI], v0[kGI], v1[kGI], v2[kGI], v3[kGI], w0[kGI], w1[kGI];
+#ifdef LZG_EXP_WTILE
+        if constexpr (LIT_LDS && RING && kGI == 1) {
+            wt_fill();
+            const uint32_t q0 = gp - 1, q = q0 + lane_id();
+            va[0] = side_byte(q, 0, wt_has(q0, 0));
+            v0[0] = side_byte(q, d0, wt_has(q0, d0)); v1[0] = side_byte(q, d1, wt_has(q0, d1));
+            v2[0] = side_byte(q, d2, wt_has(q0, d2)); v3[0] = side_byte(q, d3, wt_has(q0, d3));
+            if (with_pairs) { w0[0] = side_byte(q, e0, wt_has(q0, e0)); w1[0] = side_byte(q, e1, wt_has(q0, e1)); }
+        } else
+#endif
 #pragma unroll
         for (int it = 0; it < kGI; it++) {
             const uint32_t q = gp - 1 + (uint32_t)(it * kWave) + lane_id();
@@ -1620,6 +1664,9 @@ struct Enc {
         rpos = 0; overflow = 0; bad = 0;
         longest_found = 0; opt_end = 0; opt_cur = 0; additional_offset = 0;
         longest_len = 0; num_pairs = 0; mfpos = 0;
+#ifdef LZG_EXP_WTILE
+        wt_lo = wt_hi = 0;
+#endif
         ring_base = 0x80000000u;   // force a fill at the first read (streams < 2 GiB)
         uint32_t now_pos = 0;
         bool resumed = false;
@@ -1742,6 +1789,10 @@ __global__ void __launch_bounds__(kWave, 4) enc_kernel(EncArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t smem_s[SPEC == 1 ? kSpec1LdsBytes<(int)sizeof(PairT), LIT_LDS> : 16u];
     if constexpr (SPEC == 1) sm = smem_s;   // measured: one stream -9 %, 512 streams -10 %, 4096 flat (round 5)
     Enc<PairT, LIT_LDS, PBS, (SPEC != 0)> e;   // SPEC 1 and 2: fb <= 32, the _optimum ring
+#ifdef LZG_EXP_WTILE
+    __shared__ __attribute__((aligned(16))) uint8_t wt_s[(LIT_LDS && SPEC != 0) ? LZG_EXP_WTILE : 16];
+    e.wt = wt_s;
+#endif
     e.lane_v = threadIdx.x % kWave;
     if (SPEC == 1) {
         e.fb = 32; e.lc = 3; e.lp = 0; e.pb = 2; e.ps_mask = 3; e.eos = 0; e.tsize = 31;
