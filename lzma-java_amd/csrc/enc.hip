@@ -47,9 +47,6 @@ namespace sliced {
 constexpr bool kSliced = LZG_ENC_SLICED != 0;
 
 static __constant__ Tables c_tab = make_tables();
-#ifdef LZG_EXP_WTILE
-static __shared__ __attribute__((aligned(16))) uint8_t g_wtile[LZG_EXP_WTILE];   // the recent-window tile (experiment)
-#endif
 
 constexpr int kOptLds = 64;         // _optimum slots kept in LDS (deeper slots spill to HBM); the LDS arrays
                                     // have one more slot, kOptLds, a sink for the writes of idle lanes
@@ -212,15 +209,6 @@ struct Enc {
     const PairT* mdp;         // the current position's pairs (packed): its ring slot, or md_buf
     PairT* md_buf;            // a copy when the list is longer than the inline pairs or is clamped
     uint8_t* win;             // gather window: the cur side's bytes at offsets -1 .. kGW - 2 (aliased by tp)
-#ifdef LZG_EXP_WTILE
-    // recent-window tile (few streams per CU): an LDS ring of the stream's bytes [wt_lo, wt_hi),
-    // wt_hi - wt_lo <= kWT, kept ahead of the gather; a gathered side whose 64 bytes lie inside
-    // it reads LDS instead of the stream (InWindow.GetMatchLen, InWindow.java:120-134)
-    // v2: no state of its own (the parse is at its SGPR limit): the tile's top is a function of
-    // mfpos, hi = (mfpos / 1 KiB + 2) KiB, its bottom max(hi - kWT, 0), and a gather fills the
-    // 1 KiB chunks between the previous gather's top (gp + 1 is its mfpos) and its own
-    static constexpr uint32_t kWT = LZG_EXP_WTILE;
-#endif
     uint32_t* ring_info;      // [kRing]
     PairT* ring_pairs;        // [kRing * kInlinePairs]
     uint32_t* o_price;        // _optimum SoA, [kOptLds] each (+ the sink entry, + kFarEntry)
@@ -474,54 +462,11 @@ struct Enc {
     // equality masks per side (bit o+1 = bytes equal at offset o), keeps the three
     // bytes the position step prices its literal with in scalars and the cur side's
     // bytes in LDS (two-step literals). Compares past the window fall back to match_len.
-#ifdef LZG_EXP_WTILE
-    // the tile's top kept at least 64 bytes past the gather's last offset (1 KiB per refill,
-    // one 16-byte load per lane); a resumed slice starts the tile at its own position
-    static FI uint32_t wt_top(uint32_t m) { return ((m >> 10) + 2u) << 10; }
-    // prev_m: the previous gather's mfpos (~0u: none since the launch began)
-    FI void wt_fill(uint32_t prev_m) {
-        const uint32_t to = wt_top(mfpos);
-        uint32_t from = prev_m == ~0u ? 0u : wt_top(prev_m);
-        if (from + kWT < to) from = to - kWT;
-        for (uint32_t c = from; c < to; c += 1024u) {
-            const uint32_t o = c + lane_id() * 16u;
-            const v4u32 x = __builtin_amdgcn_raw_buffer_load_b128(inb, o, 0, 0);
-            *(v4u32*)(g_wtile + (o & (kWT - 1))) = x;
-        }
-        LANE_FENCE();
-    }
-    // the side at distance d (0 = cur) lies in the tile for all 64 lanes; the top is capped at
-    // the last whole 16-byte load inside the stream
-    FI bool wt_has(uint32_t q0, uint32_t d, uint32_t lo, uint32_t top) const {
-        return q0 >= d + lo && q0 + 63u - d < top;
-    }
-    static FI uint32_t side_tile(uint32_t q, uint32_t d) { return (uint32_t)g_wtile[(q - d) & (kWT - 1)]; }
-#endif
     FI void gather(bool with_pairs) {
-#ifdef LZG_EXP_WTILE
-        const uint32_t wt_prev = gp;
-#endif
         gp = mfpos - 1;
         const uint32_t d0 = rp0 + 1, d1 = rp1 + 1, d2 = rp2 + 1, d3 = rp3 + 1;
         const uint32_t e0 = num_pairs > 0 ? md_d(0) + 1 : d0, e1 = num_pairs > 1 ? md_d(1) + 1 : d0;
         uint32_t va[kGI], v0[kGI], v1[kGI], v2[kGI], v3[kGI], w0[kGI], w1[kGI];
-#ifdef LZG_EXP_WTILE
-        if constexpr (LIT_LDS && RING && kGI == 1) {
-            wt_fill(wt_prev + 1u);
-            const uint32_t hi = wt_top(mfpos), lo = hi > kWT ? hi - kWT : 0u;
-            const uint32_t top = hi < (n & ~15u) ? hi : (n & ~15u);
-            const uint32_t q0 = gp - 1, q = q0 + lane_id();
-            va[0] = wt_has(q0, 0, lo, top) ? side_tile(q, 0) : in_byte(q);
-            v0[0] = wt_has(q0, d0, lo, top) ? side_tile(q, d0) : in_byte(q - d0);
-            v1[0] = wt_has(q0, d1, lo, top) ? side_tile(q, d1) : in_byte(q - d1);
-            v2[0] = wt_has(q0, d2, lo, top) ? side_tile(q, d2) : in_byte(q - d2);
-            v3[0] = wt_has(q0, d3, lo, top) ? side_tile(q, d3) : in_byte(q - d3);
-            if (with_pairs) {
-                w0[0] = wt_has(q0, e0, lo, top) ? side_tile(q, e0) : in_byte(q - e0);
-                w1[0] = wt_has(q0, e1, lo, top) ? side_tile(q, e1) : in_byte(q - e1);
-            }
-        } else
-#endif
 #pragma unroll
         for (int it = 0; it < kGI; it++) {
             const uint32_t q = gp - 1 + (uint32_t)(it * kWave) + lane_id();
@@ -1675,9 +1620,6 @@ struct Enc {
         rpos = 0; overflow = 0; bad = 0;
         longest_found = 0; opt_end = 0; opt_cur = 0; additional_offset = 0;
         longest_len = 0; num_pairs = 0; mfpos = 0;
-#ifdef LZG_EXP_WTILE
-        gp = 0xFFFFFFFEu;   // no gather yet: the first one fills the tile from scratch
-#endif
         ring_base = 0x80000000u;   // force a fill at the first read (streams < 2 GiB)
         uint32_t now_pos = 0;
         bool resumed = false;
